@@ -1,0 +1,147 @@
+/*
+ * sparkts_arima.h — C ABI of the MI355X-native batched ARIMA (CSS-CGD) engine.
+ *
+ * This library is a drop-in for ONE hot path of spark-ts (dhmodi/spark-timeseries, sparkts 0.4.0-SNAPSHOT):
+ *
+ *     ARIMA.fitModel(p, d, q, ts, includeIntercept, method = "css-cgd", userInitParams)
+ *         src/main/scala/com/cloudera/sparkts/models/ARIMA.scala:79-116
+ *
+ * called once per series inside TimeSeriesRDD.mapSeries (TimeSeriesRDD.scala:249-260). The JVM binding
+ * a maintainer adds on the reference side (JNI / Panama) is shown in INTEGRATION.md; the Python mirror of
+ * python/sparkts/models/ARIMA.py lives in spark-timeseries_amd/sparkts_amd/.
+ *
+ * Conventions
+ *   - Plain C types only. Host-buffer entry points take caller-owned host memory; the library never keeps a
+ *     pointer after return. `*_device` entry points take device (HBM) pointers and a hipStream_t passed as
+ *     `void*` (NULL = the handle's own stream) and are asynchronous w.r.t. the host.
+ *   - A batch is N series of equal length T, series-major: element t of series i is series[i*ld + t]
+ *     (ld == T for the host-buffer entry points). One call = one Spark partition bucketed by length.
+ *   - Coefficient layout per series is the reference's: [c?, phi_1..phi_p, theta_1..theta_q]
+ *     (ARIMA.scala:74-77, 406); k = arima_num_params(p, q, include_intercept).
+ *   - Return value: ARIMA_OK or a negative ARIMA_E_* (API misuse / device failure only). Per-series
+ *     outcomes are reported in status_out (ARIMA_ST_*), one code per exception the reference can throw on
+ *     this path; a failed series never aborts the batch and its coefficients are NaN.
+ */
+#ifndef SPARKTS_ARIMA_H
+#define SPARKTS_ARIMA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- call-level return codes ---------------------------------------------------------------------- */
+#define ARIMA_OK              0
+#define ARIMA_E_INVALID_ARG  (-1)
+#define ARIMA_E_UNSUPPORTED  (-2)
+#define ARIMA_E_DEVICE       (-3)
+#define ARIMA_E_OOM          (-4)
+
+/* ---- per-series status: one code per reference outcome ----------------- */
+#define ARIMA_ST_OK                  0  /* fit returned normally                                             */
+#define ARIMA_ST_MAX_EVAL            1  /* commons TooManyEvaluationsException, MaxEval(10000) ARIMA.scala:196 */
+#define ARIMA_ST_BRACKET_MAX_EVAL    2  /* commons BracketFinder's own 500-evaluation cap                    */
+#define ARIMA_ST_MAX_ITER            3  /* commons TooManyIterationsException, MaxIter(10000) ARIMA.scala:195 */
+#define ARIMA_ST_SINGULAR            4  /* commons SingularMatrixException (QR rDiag == 0), ARIMA.scala:240   */
+#define ARIMA_ST_NOT_ENOUGH_DATA     5  /* MathIllegalArgumentException: rows < predictors + 1               */
+#define ARIMA_ST_NO_DATA             6  /* NoDataException: zero rows, or zero columns without intercept     */
+#define ARIMA_ST_BAD_INTERVAL        7  /* NumberIsTooLarge / OutOfRange from SearchInterval (line search)   */
+#define ARIMA_ST_ZERO_PARAMS         8  /* k == 0 parameters (ArithmeticException / index error)             */
+#define ARIMA_ST_UNSUPPORTED_METHOD  9  /* UnsupportedOperationException, ARIMA.scala:108 (and css-bobyqa)   */
+#define ARIMA_ST_SERIES_TOO_SHORT   10  /* negative lag-matrix size (NegativeArraySize / IndexOutOfBounds)    */
+
+/* ---- fit methods (ARIMA.scala:105-109) -------------------------------------------------------------- */
+#define ARIMA_METHOD_CSS_CGD     0
+#define ARIMA_METHOD_CSS_BOBYQA  1      /* recognised, not implemented: series status ARIMA_ST_UNSUPPORTED_METHOD */
+
+/* ---- stationarity / invertibility flags (ARIMAModel.isStationary / isInvertible, ARIMA.scala:777-815) - */
+#define ARIMA_FLAG_STATIONARY  1u
+#define ARIMA_FLAG_INVERTIBLE  2u
+
+typedef struct arima_handle arima_handle;
+
+/* Aggregate counters of the last fit call on a handle (for roofline accounting). */
+typedef struct arima_fit_stats {
+    int64_t n_series;
+    int64_t f_passes;        /* objective (CSS) passes actually executed over a series            */
+    int64_t g_passes;        /* gradient passes actually executed over a series (each also yields CSS) */
+    int64_t hr_passes;       /* Hannan-Rissanen streaming-QR passes executed                       */
+    int64_t n_eval;          /* objective evaluations as counted by the reference (incl. memoised)  */
+    int64_t n_grad;          /* gradient evaluations as counted by the reference                    */
+    double  flops;           /* algorithmic flops of all passes executed (SURVEY.md 8(d) formula)   */
+    double  ms_difference;   /* device time of each kernel of the last call (HIP events, ms)        */
+    double  ms_hr_init;
+    double  ms_cg_fit;
+    double  ms_total;
+} arima_fit_stats;
+
+/* ---- lifecycle ------------------------------------------------------------------------------------- */
+/* One handle per device. Calls on one handle are serialised internally (thread-safe). */
+int         arima_create(int device, arima_handle **out);
+int         arima_destroy(arima_handle *h);
+const char *arima_last_error(const arima_handle *h);
+const char *arima_status_name(int status);
+int         arima_num_params(int p, int q, int include_intercept);
+int         arima_get_last_stats(const arima_handle *h, arima_fit_stats *out);
+/* Tuning knob for the in-kernel scheduler (0 = default). Not part of the reference contract. */
+int         arima_set_option(arima_handle *h, const char *name, int64_t value);
+
+/* ---- ARIMA.fitModel over a batch (ARIMA.scala:79-116) ----------------------------------------------- *
+ * series    N x T host, series-major                 user_init  NULL (Hannan-Rissanen, ARIMA.scala:216) or N x k
+ * coef_out  N x k                                    css_ll_out N: logLikelihoodCSS at coef_out (ARIMA.scala:417)
+ * status_out N (ARIMA_ST_*)                          n_eval_out / n_grad_out: N, nullable (reference counters)
+ * flags_out N, nullable (ARIMA_FLAG_*)                                                                     */
+int arima_fit_batch(arima_handle *h, const double *series, int64_t n_series, int32_t T,
+                    int32_t p, int32_t d, int32_t q, int32_t include_intercept, int32_t method,
+                    const double *user_init, double *coef_out, double *css_ll_out, int32_t *status_out,
+                    int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out);
+
+/* Same, device-resident: every pointer is device memory; `ld` is the row stride (elements) of d_series. */
+int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_series, int32_t T, int64_t ld,
+                           int32_t p, int32_t d, int32_t q, int32_t include_intercept, int32_t method,
+                           const double *d_user_init, double *d_coef_out, double *d_css_ll_out,
+                           int32_t *d_status_out, int32_t *d_n_eval_out, int32_t *d_n_grad_out,
+                           uint8_t *d_flags_out, void *stream);
+
+/* ---- building blocks of the path (each mirrors one reference function; host buffers) --------------- */
+/* UnivariateTimeSeries.differencesOfOrderD (UnivariateTimeSeries.scala:468-480): size-preserving, N x T out */
+int arima_difference_batch(arima_handle *h, const double *series, int64_t n_series, int32_t T, int32_t d,
+                           double *out);
+/* UnivariateTimeSeries.inverseDifferencesOfOrderD (UnivariateTimeSeries.scala:489-495), N x T out */
+int arima_inverse_difference_batch(arima_handle *h, const double *series, int64_t n_series, int32_t T,
+                                   int32_t d, double *out);
+/* ARIMAModel.logLikelihoodCSS (ARIMA.scala:417-420): differences to order d, drops d, CSS log-likelihood */
+int arima_css_loglik_batch(arima_handle *h, const double *series, int64_t n_series, int32_t T,
+                           int32_t p, int32_t d, int32_t q, int32_t include_intercept, const double *coef,
+                           double *ll_out);
+/* ARIMAModel.gradientlogLikelihoodCSSARMA (ARIMA.scala:465-534) on already-differenced series (length n) */
+int arima_css_gradient_batch(arima_handle *h, const double *diffed, int64_t n_series, int32_t n,
+                             int32_t p, int32_t q, int32_t include_intercept, const double *coef,
+                             double *grad_out);
+/* ARIMA.hannanRissanenInit (ARIMA.scala:216-242) on already-differenced series (length n), N x k out */
+int arima_hannan_rissanen_batch(arima_handle *h, const double *diffed, int64_t n_series, int32_t n,
+                                int32_t p, int32_t q, int32_t include_intercept, double *init_out,
+                                int32_t *status_out);
+/* ARIMAModel.forecast (ARIMA.scala:696-764): N x (T + n_future) out */
+int arima_forecast_batch(arima_handle *h, const double *series, int64_t n_series, int32_t T,
+                         int32_t p, int32_t d, int32_t q, int32_t include_intercept, const double *coef,
+                         int32_t n_future, double *out);
+/* ARIMAModel.isStationary / isInvertible (ARIMA.scala:777-815) for N coefficient rows, flags_out N */
+int arima_model_flags_batch(arima_handle *h, const double *coef, int64_t n_series, int32_t p, int32_t q,
+                            int32_t include_intercept, uint8_t *flags_out);
+
+/* ---- synthetic workload generator (ARIMAModel.sample semantics, ARIMA.scala:655-678) ---------------- *
+ * Writes N x T series (row stride ld) into device memory: per-series coefficients = base +/- U(0, jitter)
+ * (redrawn until stationary and invertible), Philox4x32-10 + Box-Muller N(0,1) noise keyed by (seed,
+ * first_series + i, t). Deterministic for a given (seed, global series id) whatever the sharding.           */
+int arima_sample_batch_device(arima_handle *h, double *d_series, int64_t n_series, int32_t T, int64_t ld,
+                              int32_t p, int32_t d, int32_t q, int32_t include_intercept,
+                              const double *base_coef, double jitter, uint64_t seed, int64_t first_series,
+                              void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SPARKTS_ARIMA_H */

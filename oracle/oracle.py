@@ -1,0 +1,237 @@
+"""ctypes wrapper of the CPU restatement (oracle/arima_oracle.c) — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module, as the checker or
+as the timed CPU baseline; the product path (spark-timeseries_amd/) never does.
+
+Parity pinning: see the header of arima_oracle.c. The functions here add the stationarity / invertibility
+oracle, restated the way the reference computes it: eigenvalues of the companion matrix (ARIMA.findRoots,
+ARIMA.scala:381-399, commons EigenDecomposition) and `!roots.exists(_.abs() <= 1.0)` (ARIMA.scala:812-815).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libarima_oracle.so")
+_lib = None
+
+ST_NAMES = {0: "OK", 1: "MAX_EVAL", 2: "BRACKET_MAX_EVAL", 3: "MAX_ITER", 4: "SINGULAR",
+            5: "NOT_ENOUGH_DATA", 6: "NO_DATA", 7: "BAD_INTERVAL", 8: "ZERO_PARAMS",
+            9: "UNSUPPORTED_METHOD", 10: "SERIES_TOO_SHORT"}
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int)
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        L.orc_log.restype = ctypes.c_double
+        L.orc_log.argtypes = [ctypes.c_double]
+        L.orc_loglik_css_arma.restype = ctypes.c_double
+        L.orc_loglik_css_arma.argtypes = [_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp]
+        L.orc_gradient_css_arma.restype = None
+        L.orc_gradient_css_arma.argtypes = [_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp,
+                                            ctypes.c_int, _dp]
+        L.orc_differences_of_order_d.argtypes = [_dp, ctypes.c_int, ctypes.c_int, _dp]
+        L.orc_inverse_differences_of_order_d.argtypes = [_dp, ctypes.c_int, ctypes.c_int, _dp]
+        L.orc_ols.restype = ctypes.c_int
+        L.orc_ols.argtypes = [_dp, _dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp]
+        L.orc_ar_fit.restype = ctypes.c_int
+        L.orc_ar_fit.argtypes = [_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp, _dp]
+        L.orc_hannan_rissanen.restype = ctypes.c_int
+        L.orc_hannan_rissanen.argtypes = [_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp]
+        L.orc_fit.restype = ctypes.c_int
+        L.orc_fit.argtypes = [_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                              ctypes.c_int, _dp, ctypes.c_int, _dp, _dp, _ip]
+        L.orc_fit_batch.restype = ctypes.c_int
+        L.orc_fit_batch.argtypes = [_dp, ctypes.c_longlong, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp, ctypes.c_int, _dp, _dp, _ip,
+                                    _ip]
+        L.orc_forecast.argtypes = [_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   _dp, ctypes.c_int, _dp]
+        L.orc_add_time_dependent_effects.argtypes = [_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                     ctypes.c_int, ctypes.c_int, _dp, _dp]
+        L.orc_remove_time_dependent_effects.argtypes = [_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                        ctypes.c_int, ctypes.c_int, _dp, _dp]
+        _lib = L
+    return _lib
+
+
+def _c(a):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    return a, a.ctypes.data_as(_dp)
+
+
+def log(x):
+    return lib().orc_log(float(x))
+
+
+def differences_of_order_d(ts, d):
+    ts, pt = _c(ts)
+    out = np.empty_like(ts)
+    lib().orc_differences_of_order_d(pt, len(ts), d, out.ctypes.data_as(_dp))
+    return out
+
+
+def inverse_differences_of_order_d(ts, d):
+    ts, pt = _c(ts)
+    out = np.empty_like(ts)
+    lib().orc_inverse_differences_of_order_d(pt, len(ts), d, out.ctypes.data_as(_dp))
+    return out
+
+
+def loglik_css_arma(diffed, p, q, intercept, coef):
+    y, py = _c(diffed)
+    c, pc = _c(coef)
+    return lib().orc_loglik_css_arma(py, len(y), p, q, int(intercept), pc)
+
+
+def loglik_css(ts, p, d, q, intercept, coef):
+    """ARIMAModel.logLikelihoodCSS (ARIMA.scala:417-420)."""
+    return loglik_css_arma(differences_of_order_d(ts, d)[d:], p, q, intercept, coef)
+
+
+def gradient_css_arma(diffed, p, q, intercept, coef, smear=0):
+    y, py = _c(diffed)
+    c, pc = _c(coef)
+    g = np.empty(len(c))
+    lib().orc_gradient_css_arma(py, len(y), p, q, int(intercept), pc, int(smear), g.ctypes.data_as(_dp))
+    return g
+
+
+def ols(Y, X, intercept):
+    Y, py = _c(Y)
+    X = np.ascontiguousarray(X, dtype=np.float64).reshape(len(Y), -1)
+    beta = np.empty(X.shape[1] + (1 if intercept else 0) + 1)
+    st = lib().orc_ols(py, X.ctypes.data_as(_dp), len(Y), X.shape[1], int(intercept), beta.ctypes.data_as(_dp))
+    return st, beta[: X.shape[1] + (1 if intercept else 0)]
+
+
+def ar_fit(ts, max_lag, no_intercept=False):
+    ts, pt = _c(ts)
+    c = ctypes.c_double()
+    coef = np.empty(max(max_lag, 1))
+    st = lib().orc_ar_fit(pt, len(ts), max_lag, int(no_intercept), ctypes.byref(c), coef.ctypes.data_as(_dp))
+    return st, c.value, coef[:max_lag]
+
+
+def hannan_rissanen(diffed, p, q, intercept):
+    y, py = _c(diffed)
+    k = p + q + (1 if intercept else 0)
+    out = np.empty(max(k, 1))
+    st = lib().orc_hannan_rissanen(py, len(y), p, q, int(intercept), out.ctypes.data_as(_dp))
+    return st, out[:k]
+
+
+def fit(ts, p, d, q, intercept=True, method=0, user_init=None, smear=0):
+    """ARIMA.fitModel restated. Returns dict(status, coef, ll, n_eval, n_grad, n_iter)."""
+    ts, pt = _c(ts)
+    k = p + q + (1 if intercept else 0)
+    coef = np.empty(max(k, 1))
+    ll = ctypes.c_double()
+    cnt = (ctypes.c_int * 3)()
+    ui = None
+    if user_init is not None:
+        ui_arr, ui = _c(user_init)
+    st = lib().orc_fit(pt, len(ts), p, d, q, int(intercept), int(method), ui, int(smear),
+                       coef.ctypes.data_as(_dp), ctypes.byref(ll), cnt)
+    return dict(status=st, coef=coef[:k], ll=ll.value, n_eval=cnt[0], n_grad=cnt[1], n_iter=cnt[2])
+
+
+def fit_batch(series, p, d, q, intercept=True, method=0, user_init=None, smear=0, threads=None):
+    """Batch of fits (OpenMP over series). series: (N, T) float64. Returns (status, coef, ll, counters)."""
+    series = np.ascontiguousarray(series, dtype=np.float64)
+    N, T = series.shape
+    k = p + q + (1 if intercept else 0)
+    coef = np.empty((N, max(k, 1)))
+    if k == 0:
+        coef = np.empty((N, 1))
+    coef_k = np.empty((N, k)) if k else np.empty((N, 0))
+    ll = np.empty(N)
+    status = np.empty(N, dtype=np.int32)
+    counters = np.empty((N, 3), dtype=np.int32)
+    ui = None
+    if user_init is not None:
+        ui_arr = np.ascontiguousarray(user_init, dtype=np.float64).reshape(N, k)
+        ui = ui_arr.ctypes.data_as(_dp)
+    if threads is not None:
+        os.environ["OMP_NUM_THREADS"] = str(threads)
+    buf = np.empty((N, k)) if k else np.empty((N, 1))
+    lib().orc_fit_batch(series.ctypes.data_as(_dp), N, T, p, d, q, int(intercept), int(method), ui, int(smear),
+                        buf.ctypes.data_as(_dp), ll.ctypes.data_as(_dp), status.ctypes.data_as(_ip),
+                        counters.ctypes.data_as(_ip))
+    coef_k[:] = buf[:, :k]
+    return status, coef_k, ll, counters
+
+
+def forecast(ts, p, d, q, intercept, coef, n_future):
+    ts, pt = _c(ts)
+    c, pc = _c(coef)
+    out = np.empty(len(ts) + n_future)
+    lib().orc_forecast(pt, len(ts), p, d, q, int(intercept), pc, n_future, out.ctypes.data_as(_dp))
+    return out
+
+
+def add_time_dependent_effects(ts, p, d, q, intercept, coef):
+    ts, pt = _c(ts)
+    c, pc = _c(coef)
+    out = np.empty_like(ts)
+    lib().orc_add_time_dependent_effects(pt, len(ts), p, d, q, int(intercept), pc, out.ctypes.data_as(_dp))
+    return out
+
+
+def remove_time_dependent_effects(ts, p, d, q, intercept, coef):
+    ts, pt = _c(ts)
+    c, pc = _c(coef)
+    out = np.empty_like(ts)
+    lib().orc_remove_time_dependent_effects(pt, len(ts), p, d, q, int(intercept), pc, out.ctypes.data_as(_dp))
+    return out
+
+
+# ---- stationarity / invertibility: ARIMA.findRoots (companion-matrix eigenvalues), ARIMA.scala:381-399 ----
+def find_roots(coefficients):
+    c = np.asarray(coefficients, dtype=np.float64)
+    n = len(c) - 1
+    if n < 1:
+        return np.zeros(0, dtype=complex)
+    comp = np.zeros((n, n))
+    a = c[n]
+    comp[n - 1, :] = -c[:n] / a
+    if n > 1:
+        comp[: n - 1, 1:] = np.eye(n - 1)
+    return np.linalg.eigvals(comp)
+
+
+def _all_roots_outside_unit_circle(poly):
+    roots = find_roots(poly)
+    return not np.any(np.abs(roots) <= 1.0)
+
+
+def is_stationary(coef, p, q, intercept):
+    """ARIMAModel.isStationary, ARIMA.scala:777-785."""
+    if p == 0:
+        return True
+    off = 1 if intercept else 0
+    return _all_roots_outside_unit_circle(np.concatenate([[1.0], -np.asarray(coef[off:off + p])]))
+
+
+def is_invertible(coef, p, q, intercept):
+    """ARIMAModel.isInvertible, ARIMA.scala:795-803."""
+    if q == 0:
+        return True
+    off = 1 if intercept else 0
+    return _all_roots_outside_unit_circle(np.concatenate([[1.0], np.asarray(coef[off + p:])]))
+
+
+def model_flags(coef, p, q, intercept):
+    return (1 if is_stationary(coef, p, q, intercept) else 0) | (2 if is_invertible(coef, p, q, intercept) else 0)

@@ -1,0 +1,254 @@
+// arima_kernels.hip — non-template kernels (differencing, generator) and the p-dispatch of the launchers.
+// The order-specialised kernels live in arima_kernels_impl.hpp and are instantiated one AR order p per
+// translation unit (arima_inst_p0..5.hip) so the build compiles in parallel.
+#include "arima_kernels_impl.hpp"
+
+namespace sts {
+
+// =======================================================================================================
+// differencing
+// =======================================================================================================
+constexpr int kMaxD = 16;
+
+// D(i, t) = t < i ? D(i-1, t) : D(i-1, t) - D(i-1, t-1), D(0, t) = ts(t)   (UnivariateTimeSeries.scala:384-480)
+__global__ __launch_bounds__(256) void k_difference(const double *__restrict__ in, int64_t ld_in,
+                                                    double *__restrict__ out, int64_t ld_out, int64_t N, int T,
+                                                    int d, int drop) {
+    const int64_t total = N * (int64_t)T;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = idx / T;
+        const int t = (int)(idx - i * T);
+        if (drop && t < d) continue;
+        const double *row = in + i * ld_in;
+        double v[kMaxD + 1];
+#pragma unroll
+        for (int j = 0; j <= kMaxD; ++j) {
+            const int tt = t - d + j;
+            v[j] = (j <= d && tt >= 0) ? row[tt] : 0.0;
+        }
+        for (int lvl = 1; lvl <= d; ++lvl) {
+            // positions t' = t - d + j, updated only for j >= lvl (higher levels never need lower j)
+            for (int j = d; j >= lvl; --j) {
+                const int tp = t - d + j;
+                if (tp >= lvl) v[j] = v[j] - v[j - 1];
+            }
+        }
+        double r = v[0];
+#pragma unroll
+        for (int j = 0; j <= kMaxD; ++j)
+            if (j == d) r = v[j];
+        out[i * ld_out + (drop ? t - d : t)] = r;
+    }
+}
+
+// inverseDifferencesOfOrderD (UnivariateTimeSeries.scala:489-495): in-place prefix sums, one lane per series
+__global__ __launch_bounds__(256) void k_inverse_difference(const double *__restrict__ in, int64_t ld_in,
+                                                            double *__restrict__ out, int64_t ld_out,
+                                                            int64_t N, int T, int d) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const double *src = in + i * ld_in;
+    double *dst = out + i * ld_out;
+    for (int t = 0; t < T; ++t) dst[t] = src[t];
+    for (int lvl = d; lvl >= 1; --lvl)
+        for (int t = lvl; t < T; ++t) dst[t] = dst[t] + dst[t - 1];
+}
+
+// =======================================================================================================
+// Synthetic generator: ARIMAModel.sample (ARIMA.scala:655-678) with per-series jittered coefficients
+// =======================================================================================================
+constexpr int kSampleMaxOrder = 8;
+
+__device__ bool sample_roots_ok(const double *poly, int N) {   // runtime-order Schur-Cohn (see model_flags)
+    double a[kSampleMaxOrder + 1], b[kSampleMaxOrder + 1];
+    for (int i = 0; i <= N; ++i) a[i] = poly[i];
+    for (int mm = N; mm >= 1; --mm) {
+        const double kk = a[mm];
+        if (!(fabs(kk) < 1.0)) return false;
+        const double den = 1.0 - kk * kk;
+        for (int i = 0; i < mm; ++i) b[i] = (a[i] - kk * a[mm - i]) / den;
+        for (int i = 0; i < mm; ++i) a[i] = b[i];
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_sample(double *__restrict__ out, int64_t ld, int64_t N, int T, int p,
+                                                int d, int q, int I, const double *__restrict__ base,
+                                                double jitter, uint64_t seed, int64_t first) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const uint64_t gsid = (uint64_t)(first + i);
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    const int K = I + p + q, M = p > q ? p : q;
+    double c[1 + 2 * kSampleMaxOrder];
+    for (int j = 0; j < K; ++j) c[j] = base[j];
+    for (int attempt = 0; attempt < 16; ++attempt) {
+        double trial[1 + 2 * kSampleMaxOrder];
+        for (int j = 0; j < K; j += 2) {
+            uint32_t ctr[4] = {(uint32_t)j, (uint32_t)gsid, (uint32_t)(gsid >> 32), 0x5A17u + (uint32_t)attempt};
+            philox4x32_10(ctr, k0 ^ 0x3C6EF372u, k1 ^ 0xA54FF53Au);
+            trial[j] = base[j] + jitter * (2.0 * u01_53(ctr[0], ctr[1]) - 1.0);
+            if (j + 1 < K) trial[j + 1] = base[j + 1] + jitter * (2.0 * u01_53(ctr[2], ctr[3]) - 1.0);
+        }
+        double poly[kSampleMaxOrder + 1];
+        poly[0] = 1.0;
+        for (int j = 0; j < p; ++j) poly[1 + j] = -trial[I + j];
+        bool ok = sample_roots_ok(poly, p);
+        for (int j = 0; j < q; ++j) poly[1 + j] = trial[I + p + j];
+        ok = ok && sample_roots_ok(poly, q);
+        if (ok) {
+            for (int j = 0; j < K; ++j) c[j] = trial[j];
+            break;
+        }
+    }
+    // addTimeDependentEffects(noise): changes = [c]*M ++ noise; iterateARMA(changes, changes, +, errors = copy)
+    const double ia = I ? c[0] : 0.0;
+    double hist[kSampleMaxOrder];   // hist[j] = changes(i - 1 - j)
+    double ma[kSampleMaxOrder];
+    for (int j = 0; j < kSampleMaxOrder; ++j) { hist[j] = ia; ma[j] = 0.0; }
+    double *row = out + i * ld;
+    double z1 = 0.0;
+    for (int t = 0; t < T; ++t) {
+        double z;
+        if ((t & 1) == 0) {
+            uint32_t ctr[4] = {(uint32_t)(t >> 1), (uint32_t)gsid, (uint32_t)(gsid >> 32), 0xB0B0u};
+            philox4x32_10(ctr, k0, k1);
+            const double u1 = 1.0 - u01_53(ctr[0], ctr[1]);           // (0, 1]
+            const double u2 = u01_53(ctr[2], ctr[3]);
+            const double r = sqrt(-2.0 * log(u1));
+            const double ang = 6.283185307179586 * u2;
+            z = r * cos(ang);
+            z1 = r * sin(ang);
+        } else {
+            z = z1;
+        }
+        double v = z;                                     // dest(i) starts as the noise value
+        v = v + (double)I * c[0];
+        for (int j = 0; j < p; ++j) v = v + hist[j] * c[I + j];
+        for (int j = 0; j < q; ++j) v = v + ma[j] * c[I + p + j];
+        for (int j = 0; j < q - 1; ++j) ma[j + 1] = ma[j];     // updateMAErrors (ascending copy)
+        if (q > 0) ma[0] = z;                                  // error = errors(i) = the noise
+        for (int j = (M > 0 ? M : 1) - 1; j >= 1; --j) hist[j] = hist[j - 1];
+        hist[0] = v;
+        row[t] = v;
+    }
+    for (int lvl = d; lvl >= 1; --lvl)                             // inverseDifferencesOfOrderD
+        for (int t = lvl; t < T; ++t) row[t] = row[t] + row[t - 1];
+}
+
+
+// =======================================================================================================
+// launchers
+// =======================================================================================================
+int launch_difference(const double *in, int64_t ld_in, double *out, int64_t ld_out, int64_t N, int T, int d,
+                      int drop, hipStream_t s) {
+    if (d > kMaxD) return ARIMA_E_UNSUPPORTED;
+    const int64_t total = N * (int64_t)T;
+    if (total == 0) return ARIMA_OK;
+    const int64_t blocks = (total + 255) / 256;
+    const unsigned grid = (unsigned)(blocks < 65536 * 8 ? blocks : 65536 * 8);
+    hipLaunchKernelGGL(k_difference, dim3(grid), dim3(256), 0, s, in, ld_in, out, ld_out, N, T, d, drop);
+    STS_CHECK_LAUNCH();
+    return ARIMA_OK;
+}
+
+int launch_inverse_difference(const double *in, int64_t ld_in, double *out, int64_t ld_out, int64_t N, int T,
+                              int d, hipStream_t s) {
+    if (N == 0) return ARIMA_OK;
+    hipLaunchKernelGGL(k_inverse_difference, dim3(grid_for(N, 256)), dim3(256), 0, s, in, ld_in, out, ld_out, N,
+                       T, d);
+    STS_CHECK_LAUNCH();
+    return ARIMA_OK;
+}
+
+int launch_sample(double *out, int64_t ld, int64_t N, int T, int p, int d, int q, int I, const double *base,
+                  double jitter, uint64_t seed, int64_t first, hipStream_t s) {
+    if (N == 0) return ARIMA_OK;
+    if (p > kSampleMaxOrder || q > kSampleMaxOrder) return ARIMA_E_UNSUPPORTED;
+    hipLaunchKernelGGL(k_sample, dim3(grid_for(N, 256)), dim3(256), 0, s, out, ld, N, T, p, d, q, I, base, jitter,
+                       seed, first);
+    STS_CHECK_LAUNCH();
+    return ARIMA_OK;
+}
+
+STS_DECLARE_P(0, extern)
+STS_DECLARE_P(1, extern)
+STS_DECLARE_P(2, extern)
+STS_DECLARE_P(3, extern)
+STS_DECLARE_P(4, extern)
+STS_DECLARE_P(5, extern)
+
+#define STS_P_SWITCH(CALL)                                                                                 \
+    switch (p) {                                                                                           \
+    case 0: return CALL(0);                                                                                \
+    case 1: return CALL(1);                                                                                \
+    case 2: return CALL(2);                                                                                \
+    case 3: return CALL(3);                                                                                \
+    case 4: return CALL(4);                                                                                \
+    case 5: return CALL(5);                                                                                \
+    default: return ARIMA_E_UNSUPPORTED;                                                                   \
+    }
+
+int launch_hr_init(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, double *init_out,
+                   int32_t *status_out, hipStream_t s) {
+    if (N == 0) return ARIMA_OK;
+#define C_(PP) launch_hr_init_P<PP>(y, ld, n, N, q, I, init_out, status_out, s)
+    STS_P_SWITCH(C_)
+#undef C_
+}
+
+int launch_ar_fit(const double *y, int64_t ld, int n, int64_t N, int p, int I, double *coef_out, double *ll_out,
+                  int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
+                  hipStream_t s) {
+    if (N == 0) return ARIMA_OK;
+#define C_(PP) launch_ar_fit_P<PP>(y, ld, n, N, I, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out, s)
+    STS_P_SWITCH(C_)
+#undef C_
+}
+
+int launch_cg_fit(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, int smear,
+                  const double *init, const int32_t *init_status, double *coef_out, double *ll_out,
+                  int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
+                  unsigned long long *ctl, int grid_blocks, hipStream_t s) {
+    if (N == 0) return ARIMA_OK;
+#define C_(PP)                                                                                             \
+    launch_cg_fit_P<PP>(y, ld, n, N, q, I, smear, init, init_status, coef_out, ll_out, status_out, n_eval_out, \
+                        n_grad_out, flags_out, ctl, grid_blocks, s)
+    STS_P_SWITCH(C_)
+#undef C_
+}
+
+int cg_fit_occupancy_blocks(int p, int q, int I, int smear) {
+#define C_(PP) cg_fit_occupancy_blocks_P<PP>(q, I, smear)
+    STS_P_SWITCH(C_)
+#undef C_
+}
+
+int launch_css_loglik(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, const double *coef,
+                      double *ll_out, hipStream_t s) {
+    if (N == 0) return ARIMA_OK;
+#define C_(PP) launch_css_loglik_P<PP>(y, ld, n, N, q, I, coef, ll_out, s)
+    STS_P_SWITCH(C_)
+#undef C_
+}
+
+int launch_css_grad(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, int smear,
+                    const double *coef, double *g_out, hipStream_t s) {
+    if (N == 0) return ARIMA_OK;
+#define C_(PP) launch_css_grad_P<PP>(y, ld, n, N, q, I, smear, coef, g_out, s)
+    STS_P_SWITCH(C_)
+#undef C_
+}
+
+int launch_model_flags(const double *coef, int64_t N, int p, int q, int I, uint8_t *flags_out, hipStream_t s) {
+    if (N == 0) return ARIMA_OK;
+#define C_(PP) launch_model_flags_P<PP>(coef, N, q, I, flags_out, s)
+    STS_P_SWITCH(C_)
+#undef C_
+}
+
+int hr_shape_status_host(int n, int p, int q, int I) { return hr_shape_status(n, p, q, I); }
+int ar_shape_status_host(int n, int p, int I) { return ar_shape_status(n, p, I); }
+
+}  // namespace sts

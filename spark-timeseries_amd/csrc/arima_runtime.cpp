@@ -1,0 +1,496 @@
+// arima_runtime.cpp — the C ABI (include/sparkts_arima.h) over the HIP kernels: one handle per device, a
+// private stream, grow-only device workspaces, per-call HIP-event timing and aggregate pass counters.
+//
+// Call flow of arima_fit_batch_device (the drop-in for ARIMA.fitModel over one Spark partition,
+// ARIMA.scala:79-116):
+//   k_difference (differencesOfOrderD(ts, d).drop(d), :88)  ->  p>0 && q==0 ? k_ar_fit (:90-96)
+//   : [k_hr_init (:99-103, unless user init)] -> k_cg_fit (fitWithCSSCGD, :105-109, :174-200)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "../../include/sparkts_arima.h"
+#include "arima_launch.hpp"
+
+namespace {
+
+struct DevBuf {
+    void *ptr = nullptr;
+    size_t bytes = 0;
+    int ensure(size_t need) {
+        if (need <= bytes) return ARIMA_OK;
+        if (ptr) hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+        if (need == 0) return ARIMA_OK;
+        if (hipMalloc(&ptr, need) != hipSuccess) return ARIMA_E_OOM;
+        bytes = need;
+        return ARIMA_OK;
+    }
+    void release() {
+        if (ptr) hipFree(ptr);
+        ptr = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T *as() const { return static_cast<T *>(ptr); }
+};
+
+constexpr int kNumEvents = 5;
+
+}  // namespace
+
+struct arima_handle {
+    int device = 0;
+    int num_cus = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[kNumEvents] = {};
+    std::mutex mu;
+    std::string err;
+    arima_fit_stats stats{};
+    int smear = 0;
+    int grid_blocks_override = 0;
+    // device workspaces
+    DevBuf diff, init, hr_status, ctl;
+    // host-API staging
+    DevBuf h_series, h_coef, h_ll, h_status, h_neval, h_ngrad, h_flags, h_uinit, h_aux;
+    unsigned long long *ctl_host = nullptr;   // pinned
+};
+
+namespace {
+
+int set_err(arima_handle *h, int code, const char *msg) {
+    if (h) h->err = msg ? msg : "";
+    return code;
+}
+
+#define HIPCHK(h, expr)                                                                                    \
+    do {                                                                                                   \
+        hipError_t e_ = (expr);                                                                            \
+        if (e_ != hipSuccess) return set_err((h), ARIMA_E_DEVICE, hipGetErrorString(e_));                  \
+    } while (0)
+
+#define RCCHK(h, expr, what)                                                                               \
+    do {                                                                                                   \
+        int rc_ = (expr);                                                                                  \
+        if (rc_ != ARIMA_OK) return set_err((h), rc_, what);                                               \
+    } while (0)
+
+inline int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+// uniform-per-call status fill (unsupported method, zero parameters, shape errors)
+__global__ void k_fill_status(int64_t N, int k, const int32_t *__restrict__ prior, int32_t code,
+                              double *__restrict__ coef_out, double *__restrict__ ll_out,
+                              int32_t *__restrict__ status_out, int32_t *__restrict__ n_eval_out,
+                              int32_t *__restrict__ n_grad_out, uint8_t *__restrict__ flags_out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    int st = code;
+    if (prior && prior[i] != ARIMA_ST_OK) st = prior[i];
+    for (int j = 0; j < k; ++j) coef_out[i * k + j] = __builtin_nan("");
+    ll_out[i] = __builtin_nan("");
+    status_out[i] = st;
+    if (n_eval_out) n_eval_out[i] = 0;
+    if (n_grad_out) n_grad_out[i] = 0;
+    if (flags_out) flags_out[i] = 0;
+}
+
+int check_orders(arima_handle *h, int p, int d, int q, int I) {
+    if (p < 0 || q < 0 || d < 0 || (I != 0 && I != 1)) return set_err(h, ARIMA_E_INVALID_ARG, "bad order");
+    if (p > 5 || q > 5) return set_err(h, ARIMA_E_UNSUPPORTED, "p, q <= 5 are compiled in this build");
+    if (d > 16) return set_err(h, ARIMA_E_UNSUPPORTED, "d <= 16");
+    return ARIMA_OK;
+}
+
+}  // namespace
+
+namespace sts {
+int hr_shape_status_host(int n, int p, int q, int I);
+}
+
+extern "C" {
+
+int arima_num_params(int p, int q, int include_intercept) { return p + q + (include_intercept ? 1 : 0); }
+
+const char *arima_status_name(int s) {
+    switch (s) {
+    case ARIMA_ST_OK: return "OK";
+    case ARIMA_ST_MAX_EVAL: return "MAX_EVAL";
+    case ARIMA_ST_BRACKET_MAX_EVAL: return "BRACKET_MAX_EVAL";
+    case ARIMA_ST_MAX_ITER: return "MAX_ITER";
+    case ARIMA_ST_SINGULAR: return "SINGULAR";
+    case ARIMA_ST_NOT_ENOUGH_DATA: return "NOT_ENOUGH_DATA";
+    case ARIMA_ST_NO_DATA: return "NO_DATA";
+    case ARIMA_ST_BAD_INTERVAL: return "BAD_INTERVAL";
+    case ARIMA_ST_ZERO_PARAMS: return "ZERO_PARAMS";
+    case ARIMA_ST_UNSUPPORTED_METHOD: return "UNSUPPORTED_METHOD";
+    case ARIMA_ST_SERIES_TOO_SHORT: return "SERIES_TOO_SHORT";
+    default: return "UNKNOWN";
+    }
+}
+
+int arima_create(int device, arima_handle **out) {
+    if (!out) return ARIMA_E_INVALID_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ARIMA_E_DEVICE;
+    arima_handle *h = new arima_handle();
+    h->device = device;
+    if (hipSetDevice(device) != hipSuccess) { delete h; return ARIMA_E_DEVICE; }
+    hipDeviceGetAttribute(&h->num_cus, hipDeviceAttributeMultiprocessorCount, device);
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) { delete h; return ARIMA_E_DEVICE; }
+    for (auto &e : h->ev) hipEventCreate(&e);
+    if (hipHostMalloc((void **)&h->ctl_host, 16 * sizeof(unsigned long long), 0) != hipSuccess) {
+        delete h;
+        return ARIMA_E_OOM;
+    }
+    *out = h;
+    return ARIMA_OK;
+}
+
+int arima_destroy(arima_handle *h) {
+    if (!h) return ARIMA_E_INVALID_ARG;
+    hipSetDevice(h->device);
+    hipStreamSynchronize(h->stream);
+    for (DevBuf *b : {&h->diff, &h->init, &h->hr_status, &h->ctl, &h->h_series, &h->h_coef, &h->h_ll,
+                      &h->h_status, &h->h_neval, &h->h_ngrad, &h->h_flags, &h->h_uinit, &h->h_aux})
+        b->release();
+    for (auto &e : h->ev) hipEventDestroy(e);
+    if (h->ctl_host) hipHostFree(h->ctl_host);
+    hipStreamDestroy(h->stream);
+    delete h;
+    return ARIMA_OK;
+}
+
+const char *arima_last_error(const arima_handle *h) { return h ? h->err.c_str() : "null handle"; }
+
+int arima_get_last_stats(const arima_handle *h, arima_fit_stats *out) {
+    if (!h || !out) return ARIMA_E_INVALID_ARG;
+    *out = h->stats;
+    return ARIMA_OK;
+}
+
+int arima_set_option(arima_handle *h, const char *name, int64_t value) {
+    if (!h || !name) return ARIMA_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (!strcmp(name, "smear")) { h->smear = value ? 1 : 0; return ARIMA_OK; }
+    if (!strcmp(name, "grid_blocks")) { h->grid_blocks_override = (int)std::max<int64_t>(0, value); return ARIMA_OK; }
+    return set_err(h, ARIMA_E_INVALID_ARG, "unknown option");
+}
+
+// ---------------------------------------------------------------------------------------------------------
+static int fit_device_locked(arima_handle *h, const double *d_series, int64_t N, int32_t T, int64_t ld, int32_t p,
+                             int32_t d, int32_t q, int32_t I, int32_t method, const double *d_user_init,
+                             double *d_coef, double *d_ll, int32_t *d_status, int32_t *d_neval, int32_t *d_ngrad,
+                             uint8_t *d_flags, hipStream_t s) {
+    RCCHK(h, check_orders(h, p, d, q, I), "orders");
+    if (N < 0 || T < 0 || ld < T) return set_err(h, ARIMA_E_INVALID_ARG, "bad shape");
+    if (!d_coef || !d_ll || !d_status) return set_err(h, ARIMA_E_INVALID_ARG, "null output");
+    HIPCHK(h, hipSetDevice(h->device));
+    const int k = I + p + q;
+    const int n = std::max(T - d, 0);
+    const int64_t ldn = round_up(std::max(n, 1), 16);
+    arima_fit_stats st{};
+    st.n_series = N;
+    h->stats = st;
+    if (N == 0) return ARIMA_OK;
+
+    RCCHK(h, h->diff.ensure((size_t)N * ldn * sizeof(double)), "workspace");
+    RCCHK(h, h->ctl.ensure(16 * sizeof(unsigned long long)), "workspace");
+    HIPCHK(h, hipMemsetAsync(h->ctl.ptr, 0, 16 * sizeof(unsigned long long), s));
+
+    HIPCHK(h, hipEventRecord(h->ev[0], s));
+    RCCHK(h, sts::launch_difference(d_series, ld, h->diff.as<double>(), ldn, N, T, d, 1, s), "difference");
+    HIPCHK(h, hipEventRecord(h->ev[1], s));
+    const double *y = h->diff.as<double>();
+
+    if (p > 0 && q == 0) {                                     // AR-only shortcut, method never checked
+        RCCHK(h, sts::launch_ar_fit(y, ldn, n, N, p, I, d_coef, d_ll, d_status, d_neval, d_ngrad, d_flags, s),
+              "ar_fit");
+        HIPCHK(h, hipEventRecord(h->ev[2], s));
+        HIPCHK(h, hipEventRecord(h->ev[3], s));
+    } else {
+        const double *init = d_user_init;
+        const int32_t *init_status = nullptr;
+        if (!d_user_init) {
+            RCCHK(h, h->init.ensure((size_t)N * std::max(k, 1) * sizeof(double)), "workspace");
+            RCCHK(h, h->hr_status.ensure((size_t)N * sizeof(int32_t)), "workspace");
+            RCCHK(h, sts::launch_hr_init(y, ldn, n, N, p, q, I, h->init.as<double>(), h->hr_status.as<int32_t>(), s),
+                  "hr_init");
+            init = h->init.as<double>();
+            init_status = h->hr_status.as<int32_t>();
+        }
+        HIPCHK(h, hipEventRecord(h->ev[2], s));
+        const unsigned grid = (unsigned)((N + 255) / 256);
+        if (method != ARIMA_METHOD_CSS_CGD || k == 0) {
+            const int32_t code = (method != ARIMA_METHOD_CSS_CGD) ? ARIMA_ST_UNSUPPORTED_METHOD : ARIMA_ST_ZERO_PARAMS;
+            hipLaunchKernelGGL(k_fill_status, dim3(grid), dim3(256), 0, s, N, k, init_status, code, d_coef, d_ll,
+                               d_status, d_neval, d_ngrad, d_flags);
+            HIPCHK(h, hipGetLastError());
+        } else {
+            int blocks = h->grid_blocks_override;
+            if (blocks <= 0) {
+                const int per_cu = std::max(1, sts::cg_fit_occupancy_blocks(p, q, I, h->smear));
+                blocks = per_cu * std::max(1, h->num_cus);
+            }
+            const int64_t need = (N + 255) / 256;
+            if (blocks > need) blocks = (int)need;
+            RCCHK(h, sts::launch_cg_fit(y, ldn, n, N, p, q, I, h->smear, init, init_status, d_coef, d_ll, d_status,
+                                        d_neval, d_ngrad, d_flags, h->ctl.as<unsigned long long>(), blocks, s),
+                  "cg_fit");
+        }
+        HIPCHK(h, hipEventRecord(h->ev[3], s));
+    }
+    HIPCHK(h, hipMemcpyAsync(h->ctl_host, h->ctl.ptr, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    float ms = 0;
+    hipEventElapsedTime(&ms, h->ev[0], h->ev[1]);
+    st.ms_difference = ms;
+    hipEventElapsedTime(&ms, h->ev[1], h->ev[2]);
+    st.ms_hr_init = ms;
+    hipEventElapsedTime(&ms, h->ev[2], h->ev[3]);
+    st.ms_cg_fit = ms;
+    hipEventElapsedTime(&ms, h->ev[0], h->ev[3]);
+    st.ms_total = ms;
+    const unsigned long long *c = h->ctl_host;
+    st.f_passes = (int64_t)c[1];
+    st.g_passes = (int64_t)c[2];
+    st.n_eval = (int64_t)c[5];
+    st.n_grad = (int64_t)c[6];
+    // HR passes: 2 per column of each of the two least squares (+1 re-transform sweep over C rows)
+    const int M = std::max(p, q), m = M + 1;
+    if (p > 0 && q == 0) st.hr_passes = N * (int64_t)(2 * (I + p));
+    else if (!d_user_init) st.hr_passes = N * (int64_t)(2 * (1 + m) + 2 * k);
+    // algorithmic flops: U*S*(2(p+q)+4) + G*S*(2(p+q)+4 + 2kq + 1+p+q + 2k) + W_HR
+    const double S = std::max(n - M, 0);
+    const double ff = 2.0 * (p + q) + 4, fg = ff + 2.0 * k * q + 1 + p + q + 2.0 * k;
+    const double whr = (double)N * (3.0 * std::max(n - m, 0) * (m + 1) * (m + 1) +
+                                    3.0 * std::max(n - 2 * M - 1, 0) * k * k + 2.0 * std::max(n - m, 0) * m);
+    st.flops = (double)st.f_passes * S * ff + (double)st.g_passes * S * fg + (d_user_init ? 0.0 : whr);
+    st.n_series = N;
+    h->stats = st;
+    return ARIMA_OK;
+}
+
+int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_series, int32_t T, int64_t ld,
+                           int32_t p, int32_t d, int32_t q, int32_t include_intercept, int32_t method,
+                           const double *d_user_init, double *d_coef_out, double *d_css_ll_out,
+                           int32_t *d_status_out, int32_t *d_n_eval_out, int32_t *d_n_grad_out,
+                           uint8_t *d_flags_out, void *stream) {
+    if (!h) return ARIMA_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    return fit_device_locked(h, d_series, n_series, T, ld, p, d, q, include_intercept, method, d_user_init,
+                             d_coef_out, d_css_ll_out, d_status_out, d_n_eval_out, d_n_grad_out, d_flags_out, s);
+}
+
+int arima_fit_batch(arima_handle *h, const double *series, int64_t N, int32_t T, int32_t p, int32_t d, int32_t q,
+                    int32_t I, int32_t method, const double *user_init, double *coef_out, double *css_ll_out,
+                    int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out) {
+    if (!h) return ARIMA_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    RCCHK(h, check_orders(h, p, d, q, I), "orders");
+    if (N < 0 || T < 0 || (N > 0 && (!series || !coef_out || !css_ll_out || !status_out)))
+        return set_err(h, ARIMA_E_INVALID_ARG, "bad arguments");
+    if (N == 0) return ARIMA_OK;
+    HIPCHK(h, hipSetDevice(h->device));
+    const int k = I + p + q;
+    const size_t kk = (size_t)std::max(k, 1);
+    hipStream_t s = h->stream;
+    RCCHK(h, h->h_series.ensure((size_t)N * std::max(T, 1) * sizeof(double)), "staging");
+    RCCHK(h, h->h_coef.ensure((size_t)N * kk * sizeof(double)), "staging");
+    RCCHK(h, h->h_ll.ensure((size_t)N * sizeof(double)), "staging");
+    RCCHK(h, h->h_status.ensure((size_t)N * sizeof(int32_t)), "staging");
+    RCCHK(h, h->h_neval.ensure((size_t)N * sizeof(int32_t)), "staging");
+    RCCHK(h, h->h_ngrad.ensure((size_t)N * sizeof(int32_t)), "staging");
+    RCCHK(h, h->h_flags.ensure((size_t)N), "staging");
+    if (T > 0) HIPCHK(h, hipMemcpyAsync(h->h_series.ptr, series, (size_t)N * T * sizeof(double), hipMemcpyHostToDevice, s));
+    const double *d_ui = nullptr;
+    if (user_init && k > 0) {
+        RCCHK(h, h->h_uinit.ensure((size_t)N * k * sizeof(double)), "staging");
+        HIPCHK(h, hipMemcpyAsync(h->h_uinit.ptr, user_init, (size_t)N * k * sizeof(double), hipMemcpyHostToDevice, s));
+        d_ui = h->h_uinit.as<double>();
+    } else if (user_init) {
+        RCCHK(h, h->h_uinit.ensure(8), "staging");
+        d_ui = h->h_uinit.as<double>();
+    }
+    int rc = fit_device_locked(h, h->h_series.as<double>(), N, T, T, p, d, q, I, method, d_ui, h->h_coef.as<double>(),
+                               h->h_ll.as<double>(), h->h_status.as<int32_t>(), h->h_neval.as<int32_t>(),
+                               h->h_ngrad.as<int32_t>(), h->h_flags.as<uint8_t>(), s);
+    if (rc != ARIMA_OK) return rc;
+    if (k > 0) HIPCHK(h, hipMemcpyAsync(coef_out, h->h_coef.ptr, (size_t)N * k * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipMemcpyAsync(css_ll_out, h->h_ll.ptr, (size_t)N * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipMemcpyAsync(status_out, h->h_status.ptr, (size_t)N * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    if (n_eval_out) HIPCHK(h, hipMemcpyAsync(n_eval_out, h->h_neval.ptr, (size_t)N * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    if (n_grad_out) HIPCHK(h, hipMemcpyAsync(n_grad_out, h->h_ngrad.ptr, (size_t)N * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    if (flags_out) HIPCHK(h, hipMemcpyAsync(flags_out, h->h_flags.ptr, (size_t)N, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    return ARIMA_OK;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// building blocks (host buffers)
+// ---------------------------------------------------------------------------------------------------------
+int arima_difference_batch(arima_handle *h, const double *series, int64_t N, int32_t T, int32_t d, double *out) {
+    if (!h || N < 0 || T < 0 || d < 0) return ARIMA_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (N == 0 || T == 0) return ARIMA_OK;
+    HIPCHK(h, hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    const size_t bytes = (size_t)N * T * sizeof(double);
+    RCCHK(h, h->h_series.ensure(bytes), "staging");
+    RCCHK(h, h->h_aux.ensure(bytes), "staging");
+    HIPCHK(h, hipMemcpyAsync(h->h_series.ptr, series, bytes, hipMemcpyHostToDevice, s));
+    RCCHK(h, sts::launch_difference(h->h_series.as<double>(), T, h->h_aux.as<double>(), T, N, T, d, 0, s), "difference");
+    HIPCHK(h, hipMemcpyAsync(out, h->h_aux.ptr, bytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    return ARIMA_OK;
+}
+
+int arima_inverse_difference_batch(arima_handle *h, const double *series, int64_t N, int32_t T, int32_t d,
+                                   double *out) {
+    if (!h || N < 0 || T < 0 || d < 0) return ARIMA_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (N == 0 || T == 0) return ARIMA_OK;
+    HIPCHK(h, hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    const size_t bytes = (size_t)N * T * sizeof(double);
+    RCCHK(h, h->h_series.ensure(bytes), "staging");
+    RCCHK(h, h->h_aux.ensure(bytes), "staging");
+    HIPCHK(h, hipMemcpyAsync(h->h_series.ptr, series, bytes, hipMemcpyHostToDevice, s));
+    RCCHK(h, sts::launch_inverse_difference(h->h_series.as<double>(), T, h->h_aux.as<double>(), T, N, T, d, s),
+          "inverse_difference");
+    HIPCHK(h, hipMemcpyAsync(out, h->h_aux.ptr, bytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    return ARIMA_OK;
+}
+
+// upload N rows of length n into the padded (ld multiple of 16) workspace h->diff
+static int upload_padded(arima_handle *h, const double *src, int64_t N, int32_t n, int64_t *ld_out, hipStream_t s) {
+    const int64_t ld = round_up(std::max(n, 1), 16);
+    RCCHK(h, h->diff.ensure((size_t)N * ld * sizeof(double)), "workspace");
+    if (n > 0)
+        HIPCHK(h, hipMemcpy2DAsync(h->diff.ptr, ld * sizeof(double), src, (size_t)n * sizeof(double),
+                                   (size_t)n * sizeof(double), N, hipMemcpyHostToDevice, s));
+    *ld_out = ld;
+    return ARIMA_OK;
+}
+
+int arima_css_loglik_batch(arima_handle *h, const double *series, int64_t N, int32_t T, int32_t p, int32_t d,
+                           int32_t q, int32_t I, const double *coef, double *ll_out) {
+    if (!h) return ARIMA_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    RCCHK(h, check_orders(h, p, d, q, I), "orders");
+    if (N < 0 || T < 0) return set_err(h, ARIMA_E_INVALID_ARG, "bad shape");
+    if (N == 0) return ARIMA_OK;
+    HIPCHK(h, hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    const int k = I + p + q;
+    const int n = std::max(T - d, 0);
+    const int64_t ldn = round_up(std::max(n, 1), 16);
+    RCCHK(h, h->h_series.ensure((size_t)N * std::max(T, 1) * sizeof(double)), "staging");
+    RCCHK(h, h->diff.ensure((size_t)N * ldn * sizeof(double)), "workspace");
+    RCCHK(h, h->h_coef.ensure((size_t)N * std::max(k, 1) * sizeof(double)), "staging");
+    RCCHK(h, h->h_ll.ensure((size_t)N * sizeof(double)), "staging");
+    if (T > 0) HIPCHK(h, hipMemcpyAsync(h->h_series.ptr, series, (size_t)N * T * sizeof(double), hipMemcpyHostToDevice, s));
+    if (k > 0) HIPCHK(h, hipMemcpyAsync(h->h_coef.ptr, coef, (size_t)N * k * sizeof(double), hipMemcpyHostToDevice, s));
+    RCCHK(h, sts::launch_difference(h->h_series.as<double>(), T, h->diff.as<double>(), ldn, N, T, d, 1, s), "difference");
+    RCCHK(h, sts::launch_css_loglik(h->diff.as<double>(), ldn, n, N, p, q, I, h->h_coef.as<double>(),
+                                    h->h_ll.as<double>(), s), "css_loglik");
+    HIPCHK(h, hipMemcpyAsync(ll_out, h->h_ll.ptr, (size_t)N * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    return ARIMA_OK;
+}
+
+int arima_css_gradient_batch(arima_handle *h, const double *diffed, int64_t N, int32_t n, int32_t p, int32_t q,
+                             int32_t I, const double *coef, double *grad_out) {
+    if (!h) return ARIMA_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    RCCHK(h, check_orders(h, p, 0, q, I), "orders");
+    if (N < 0 || n < 0) return set_err(h, ARIMA_E_INVALID_ARG, "bad shape");
+    const int k = I + p + q;
+    if (N == 0 || k == 0) return ARIMA_OK;
+    HIPCHK(h, hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    int64_t ld = 0;
+    RCCHK(h, upload_padded(h, diffed, N, n, &ld, s), "upload");
+    RCCHK(h, h->h_coef.ensure((size_t)N * k * sizeof(double)), "staging");
+    RCCHK(h, h->h_aux.ensure((size_t)N * k * sizeof(double)), "staging");
+    HIPCHK(h, hipMemcpyAsync(h->h_coef.ptr, coef, (size_t)N * k * sizeof(double), hipMemcpyHostToDevice, s));
+    RCCHK(h, sts::launch_css_grad(h->diff.as<double>(), ld, n, N, p, q, I, h->smear, h->h_coef.as<double>(),
+                                  h->h_aux.as<double>(), s), "css_grad");
+    HIPCHK(h, hipMemcpyAsync(grad_out, h->h_aux.ptr, (size_t)N * k * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    return ARIMA_OK;
+}
+
+int arima_hannan_rissanen_batch(arima_handle *h, const double *diffed, int64_t N, int32_t n, int32_t p, int32_t q,
+                                int32_t I, double *init_out, int32_t *status_out) {
+    if (!h) return ARIMA_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    RCCHK(h, check_orders(h, p, 0, q, I), "orders");
+    if (N < 0 || n < 0) return set_err(h, ARIMA_E_INVALID_ARG, "bad shape");
+    if (N == 0) return ARIMA_OK;
+    HIPCHK(h, hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    const int k = I + p + q;
+    int64_t ld = 0;
+    RCCHK(h, upload_padded(h, diffed, N, n, &ld, s), "upload");
+    RCCHK(h, h->h_coef.ensure((size_t)N * std::max(k, 1) * sizeof(double)), "staging");
+    RCCHK(h, h->h_status.ensure((size_t)N * sizeof(int32_t)), "staging");
+    RCCHK(h, sts::launch_hr_init(h->diff.as<double>(), ld, n, N, p, q, I, h->h_coef.as<double>(),
+                                 h->h_status.as<int32_t>(), s), "hr_init");
+    if (k > 0) HIPCHK(h, hipMemcpyAsync(init_out, h->h_coef.ptr, (size_t)N * k * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipMemcpyAsync(status_out, h->h_status.ptr, (size_t)N * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    return ARIMA_OK;
+}
+
+int arima_model_flags_batch(arima_handle *h, const double *coef, int64_t N, int32_t p, int32_t q, int32_t I,
+                            uint8_t *flags_out) {
+    if (!h) return ARIMA_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    RCCHK(h, check_orders(h, p, 0, q, I), "orders");
+    if (N <= 0) return ARIMA_OK;
+    HIPCHK(h, hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    const int k = I + p + q;
+    RCCHK(h, h->h_coef.ensure((size_t)N * std::max(k, 1) * sizeof(double)), "staging");
+    RCCHK(h, h->h_flags.ensure((size_t)N), "staging");
+    if (k > 0) HIPCHK(h, hipMemcpyAsync(h->h_coef.ptr, coef, (size_t)N * k * sizeof(double), hipMemcpyHostToDevice, s));
+    RCCHK(h, sts::launch_model_flags(h->h_coef.as<double>(), N, p, q, I, h->h_flags.as<uint8_t>(), s), "flags");
+    HIPCHK(h, hipMemcpyAsync(flags_out, h->h_flags.ptr, (size_t)N, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    return ARIMA_OK;
+}
+
+int arima_forecast_batch(arima_handle *h, const double *series, int64_t n_series, int32_t T, int32_t p, int32_t d,
+                         int32_t q, int32_t include_intercept, const double *coef, int32_t n_future, double *out) {
+    (void)series; (void)n_series; (void)T; (void)p; (void)d; (void)q; (void)include_intercept; (void)coef;
+    (void)n_future; (void)out;
+    return set_err(h, ARIMA_E_UNSUPPORTED, "forecast: not built yet");
+}
+
+int arima_sample_batch_device(arima_handle *h, double *d_series, int64_t N, int32_t T, int64_t ld, int32_t p,
+                              int32_t d, int32_t q, int32_t I, const double *base_coef, double jitter,
+                              uint64_t seed, int64_t first_series, void *stream) {
+    if (!h || !base_coef || N < 0 || T < 0 || ld < T) return ARIMA_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    RCCHK(h, check_orders(h, p, d, q, I), "orders");
+    HIPCHK(h, hipSetDevice(h->device));
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    const int k = I + p + q;
+    RCCHK(h, h->h_aux.ensure((size_t)std::max(k, 1) * sizeof(double)), "staging");
+    if (k > 0) HIPCHK(h, hipMemcpyAsync(h->h_aux.ptr, base_coef, (size_t)k * sizeof(double), hipMemcpyHostToDevice, s));
+    RCCHK(h, sts::launch_sample(d_series, ld, N, T, p, d, q, I, h->h_aux.as<double>(), jitter, seed, first_series, s),
+          "sample");
+    HIPCHK(h, hipStreamSynchronize(s));
+    return ARIMA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,174 @@
+"""MI355X-native mirror of python/sparkts/models/ARIMA.py (spark-ts) over the HIP engine.
+
+Same names, argument meaning and error behaviour as the reference's Python binding (which forwards to
+com.cloudera.sparkts.models.ARIMA over py4j, python/sparkts/models/ARIMA.py:62-104, 106-262); `sc` is accepted
+and ignored (there is no JVM). Where the reference throws a Java exception, the mirror raises an exception of
+the same name (subclass of ARIMAFitError). Batched entry points (`fit_models`) are the drop-in for
+TimeSeriesRDD.mapSeries over ARIMA fits (one ABI call per partition, TimeSeriesRDD.scala:249-260).
+"""
+import numpy as np
+
+from .. import _lib
+
+
+class ARIMAFitError(RuntimeError):
+    """Base of the per-series failures (status != OK)."""
+
+    status = None
+
+
+class TooManyEvaluationsException(ARIMAFitError):
+    pass
+
+
+class TooManyIterationsException(ARIMAFitError):
+    pass
+
+
+class SingularMatrixException(ARIMAFitError):
+    pass
+
+
+class MathIllegalArgumentException(ARIMAFitError):
+    pass
+
+
+class NoDataException(ARIMAFitError):
+    pass
+
+
+class NumberIsTooLargeException(ARIMAFitError):
+    pass
+
+
+class ArithmeticException(ARIMAFitError):
+    pass
+
+
+class UnsupportedOperationException(ARIMAFitError):
+    pass
+
+
+class IndexOutOfBoundsException(ARIMAFitError):
+    pass
+
+
+_EXC = {
+    _lib.ST_MAX_EVAL: TooManyEvaluationsException,
+    _lib.ST_BRACKET_MAX_EVAL: TooManyEvaluationsException,
+    _lib.ST_MAX_ITER: TooManyIterationsException,
+    _lib.ST_SINGULAR: SingularMatrixException,
+    _lib.ST_NOT_ENOUGH_DATA: MathIllegalArgumentException,
+    _lib.ST_NO_DATA: NoDataException,
+    _lib.ST_BAD_INTERVAL: NumberIsTooLargeException,
+    _lib.ST_ZERO_PARAMS: ArithmeticException,
+    _lib.ST_UNSUPPORTED_METHOD: UnsupportedOperationException,
+    _lib.ST_SERIES_TOO_SHORT: IndexOutOfBoundsException,
+}
+
+
+def raise_for_status(status):
+    if status != _lib.ST_OK:
+        exc = _EXC.get(int(status), ARIMAFitError)
+        e = exc(f"ARIMA fit failed: status {int(status)} ({_lib.load().arima_status_name(int(status)).decode()})")
+        e.status = int(status)
+        raise e
+
+
+def _method_code(method):
+    if method not in _lib.METHODS:
+        return 99      # unknown method string -> UnsupportedOperationException (ARIMA.scala:108)
+    return _lib.METHODS[method]
+
+
+def autofit(ts, maxp=5, maxd=2, maxq=5, sc=None):
+    """ARIMA.autoFit (ARIMA.scala:280-304) is outside this round's hot-path scope."""
+    raise NotImplementedError("autofit: order search is a later row of SURVEY.md 8(f)")
+
+
+def fit_model(p, d, q, ts, includeIntercept=True, method="css-cgd", userInitParams=None, sc=None, device=None):
+    """ARIMA.fitModel (ARIMA.scala:79-116), one series. Raises the reference's exception on failure."""
+    ts = np.asarray(ts, dtype=np.float64).ravel()
+    res = fit_models(p, d, q, ts[None, :], includeIntercept, method, userInitParams, device=device)
+    raise_for_status(res.status[0])
+    return ARIMAModel(p, d, q, res.coefficients[0], includeIntercept, device=device)
+
+
+class FitBatchResult:
+    """Per-series outputs of a batched fit (the arrays the C ABI fills)."""
+
+    def __init__(self, p, d, q, include_intercept, r, stats):
+        self.p, self.d, self.q, self.has_intercept = p, d, q, include_intercept
+        self.coefficients = r["coef"]
+        self.css_loglik = r["ll"]
+        self.status = r["status"]
+        self.n_eval = r["n_eval"]
+        self.n_grad = r["n_grad"]
+        self.flags = r["flags"]
+        self.stats = stats
+
+    def model(self, i):
+        raise_for_status(self.status[i])
+        return ARIMAModel(self.p, self.d, self.q, self.coefficients[i], self.has_intercept)
+
+    @property
+    def converged(self):
+        return self.status == _lib.ST_OK
+
+
+def fit_models(p, d, q, series, includeIntercept=True, method="css-cgd", userInitParams=None, device=None):
+    """Batched ARIMA.fitModel: `series` is (N, T) float64, one row per series (one Spark partition bucket).
+
+    Never raises for per-series failures; inspect `.status` (ARIMA_ST_* codes, include/sparkts_arima.h)."""
+    eng = _lib.Engine.get(device)
+    r = eng.fit_batch(series, p, d, q, includeIntercept, _method_code(method), userInitParams)
+    return FitBatchResult(p, d, q, includeIntercept, r, eng.stats())
+
+
+class ARIMAModel:
+    """ARIMAModel (ARIMA.scala:402-831) with the reference Python binding's method names."""
+
+    def __init__(self, p=0, d=0, q=0, coefficients=None, hasIntercept=True, jmodel=None, sc=None, device=None):
+        self.p, self.d, self.q = int(p), int(d), int(q)
+        self.coefficients = np.asarray(coefficients, dtype=np.float64).copy()
+        self.has_intercept = bool(hasIntercept)
+        self._device = device
+
+    @property
+    def _eng(self):
+        return _lib.Engine.get(self._device)
+
+    def log_likelihood_css(self, y):
+        """logLikelihoodCSS (ARIMA.scala:417-420)."""
+        return float(self._eng.css_loglik(np.asarray(y, dtype=np.float64)[None, :], self.p, self.d, self.q,
+                                          self.has_intercept, self.coefficients)[0])
+
+    def log_likelihood_css_arma(self, diffedy):
+        """logLikelihoodCSSARMA (ARIMA.scala:430-445) on an already differenced series."""
+        return float(self._eng.css_loglik(np.asarray(diffedy, dtype=np.float64)[None, :], self.p, 0, self.q,
+                                          self.has_intercept, self.coefficients)[0])
+
+    def gradient_log_likelihood_css_arma(self, diffedy):
+        """gradientlogLikelihoodCSSARMA (ARIMA.scala:465-534)."""
+        return self._eng.css_gradient(np.asarray(diffedy, dtype=np.float64)[None, :], self.p, self.q,
+                                      self.has_intercept, self.coefficients)[0]
+
+    def forecast(self, ts, nfuture):
+        """forecast (ARIMA.scala:696-764)."""
+        return self._eng.forecast(np.asarray(ts, dtype=np.float64)[None, :], self.p, self.d, self.q,
+                                  self.has_intercept, self.coefficients, int(nfuture))[0]
+
+    def is_stationary(self):
+        """isStationary (ARIMA.scala:777-785)."""
+        f = self._eng.model_flags(self.coefficients[None, :], self.p, self.q, self.has_intercept)[0]
+        return bool(f & _lib.FLAG_STATIONARY)
+
+    def is_invertible(self):
+        """isInvertible (ARIMA.scala:795-803)."""
+        f = self._eng.model_flags(self.coefficients[None, :], self.p, self.q, self.has_intercept)[0]
+        return bool(f & _lib.FLAG_INVERTIBLE)
+
+    def approx_aic(self, ts):
+        """approxAIC (ARIMA.scala:826-830)."""
+        k = self.p + self.q + (1 if self.has_intercept else 0)
+        return -2 * self.log_likelihood_css(ts) + 2 * k

@@ -1,0 +1,65 @@
+"""The C-ABI library loads and exports every symbol include/sparkts_arima.h declares (no GPU needed)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "sparkts_arima.h")
+
+
+def declared_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(arima_[a-z_]+)\s*\(", txt)))
+
+
+def test_header_and_binding_agree():
+    import sparkts_amd._lib as L
+    assert declared_functions() == sorted(L.EXPORTED)
+
+
+def test_library_exports_every_declared_symbol():
+    import sparkts_amd._lib as L
+    lib = L.load()
+    nm = subprocess.check_output(["nm", "-D", "--defined-only", L.LIB_PATH], text=True)
+    exported = set(re.findall(r" T (arima_\w+)", nm))
+    for name in declared_functions():
+        assert name in exported, name
+        assert hasattr(lib, name)
+
+
+def test_exports_are_plain_c_no_torch():
+    import sparkts_amd._lib as L
+    deps = subprocess.check_output(["ldd", L.LIB_PATH], text=True)
+    assert "torch" not in deps and "c10" not in deps
+
+
+def test_pure_host_entry_points():
+    import sparkts_amd._lib as L
+    lib = L.load()
+    assert lib.arima_num_params(2, 2, 1) == 5 and lib.arima_num_params(0, 0, 0) == 0
+    names = [lib.arima_status_name(i).decode() for i in range(11)]
+    assert names == ["OK", "MAX_EVAL", "BRACKET_MAX_EVAL", "MAX_ITER", "SINGULAR", "NOT_ENOUGH_DATA", "NO_DATA",
+                     "BAD_INTERVAL", "ZERO_PARAMS", "UNSUPPORTED_METHOD", "SERIES_TOO_SHORT"]
+
+
+def test_status_codes_match_oracle_numbering():
+    import oracle as O
+    import sparkts_amd._lib as L
+    lib = L.load()
+    for code, name in O.ST_NAMES.items():
+        assert lib.arima_status_name(code).decode() == name
+
+
+def test_product_path_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    import sparkts_amd._lib as L
+    from sparkts_amd.models import ARIMA
+    with pytest.raises(L.EngineError):
+        ARIMA.fit_model(1, 0, 1, [1.0, 2.0, 3.0, 5.0, 4.0, 6.0, 5.0, 7.0])
