@@ -70,12 +70,24 @@ _vp = ctypes.c_void_p
 _i32, _i64, _f64, _u64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_uint64
 
 
+def _single_hip_runtime():
+    """PyTorch-ROCm wheels bundle their own libamdhip64/libhsa-runtime64 (same SONAME as /opt/rocm's). If this
+    library were loaded first, a later `import torch` would map a SECOND HIP runtime into the process and torch
+    would see no GPU. Importing torch first makes the dynamic loader bind this library to torch's runtime, so a
+    process that also uses torch (bench.py's torch.distributed plumbing, tests) has exactly one HIP runtime."""
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 def load():
     """Load the shared library (no GPU needed). Raises if it is missing."""
     global _lib
     with _lock:
         if _lib is not None:
             return _lib
+        _single_hip_runtime()
         if not os.path.exists(LIB_PATH):
             raise EngineError(f"HIP library not built: {LIB_PATH} (run `python -c 'import __graft_entry__ as g; "
                               f"g.build()'` or `make -C spark-timeseries_amd/csrc`)")
