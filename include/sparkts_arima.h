@@ -74,6 +74,9 @@ typedef struct arima_fit_stats {
     double  ms_hr_init;
     double  ms_cg_fit;
     double  ms_total;
+    int64_t wave_f_passes;   /* wave-level objective-only passes of the fit kernel                   */
+    int64_t wave_g_passes;   /* wave-level passes that included the gradient recursion               */
+    int64_t grid_blocks;     /* workgroups of the persistent fit kernel                               */
 } arima_fit_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------------------- */

@@ -21,6 +21,7 @@ constexpr int kMaxIter = 10000;      // new MaxIter(10000)  ARIMA.scala:195
 constexpr int kBracketMax = 500;     // commons BracketFinder() = BracketFinder(growLimit 100, maxEval 500)
 constexpr int kChunk = 16;           // doubles per lane per streamed chunk (one 128-B line)
 
+
 // ------------------------------------------------------------------------------------------------------
 // fdlibm __ieee754_log (used by logLikelihoodCSSARMA, ARIMA.scala:444)
 // ------------------------------------------------------------------------------------------------------
@@ -92,19 +93,63 @@ __device__ __forceinline__ double css_to_loglik(double css, int n) {
 __device__ __forceinline__ bool finite(double v) { return __builtin_isfinite(v); }
 
 // ------------------------------------------------------------------------------------------------------
-// Per-lane streaming reader over one series row (128-B aligned), one 128-B line (16 doubles) per refill.
+// Per-lane streaming of one series row. Every lane walks its own row front to back, so a wave touches 64
+// different 128-B lines per load instruction; each lane therefore fetches whole lines (8 x 16-B loads = one
+// 128-B chunk) and keeps D chunks in flight in registers (chunk c+D is requested while chunk c is consumed).
+// The unaligned head (up to the first 16-element boundary) and the tail use single loads, so the unrolled body
+// has no guards.
 // ------------------------------------------------------------------------------------------------------
 struct Chunk {
     double v[kChunk];
 };
 
-__device__ __forceinline__ void load_chunk(const double *__restrict__ row, int c, Chunk &out) {
-    const double2 *p = reinterpret_cast<const double2 *>(row + c * kChunk);
+__device__ __forceinline__ void load_chunk(const double *__restrict__ p, Chunk &out) {
+    const double2 *q = reinterpret_cast<const double2 *>(p);
 #pragma unroll
     for (int u = 0; u < kChunk / 2; ++u) {
-        double2 t = p[u];
+        const double2 t = q[u];
         out.v[2 * u] = t.x;
         out.v[2 * u + 1] = t.y;
+    }
+}
+
+// fn(row[i]) for i = first .. last-1, in order. `row` must be 128-B aligned and readable over the 128-B
+// chunks that contain first .. last-1. Every chunk of the range is fetched whole; loads are UNCONDITIONAL
+// (refills past the end re-read the last chunk, an L2 hit) so no control-flow join ever merges a load result
+// (a join would force s_waitcnt vmcnt(0) and kill the prefetch). Only the first and the last chunk test the
+// element range.
+template <int D, class Fn>
+__device__ __forceinline__ void stream_elems(const double *__restrict__ row, int first, int last, Fn &&fn) {
+    if (first >= last) return;
+    const int c_first = first / kChunk;
+    const int c_last = (last - 1) / kChunk;
+    const int nch = c_last - c_first + 1;
+    const double *base = row + c_first * kChunk;
+    Chunk ring[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) load_chunk(base + (j < nch ? j : nch - 1) * kChunk, ring[j]);
+    const int head = first - c_first * kChunk;          // elements of chunk 0 before `first`
+    const int tail = last - c_last * kChunk;            // elements of the last chunk that are in range
+    for (int c0 = 0; c0 < nch; c0 += D) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            const int ch = c0 + j;
+            if (ch < nch) {
+                const bool full = (ch > 0 || head == 0) && (ch < nch - 1 || tail == kChunk);
+                if (full) {
+#pragma unroll
+                    for (int u = 0; u < kChunk; ++u) fn(ring[j].v[u]);
+                } else {
+                    const int lo = (ch == 0) ? head : 0;
+                    const int hi = (ch == nch - 1) ? tail : kChunk;
+#pragma unroll
+                    for (int u = 0; u < kChunk; ++u)
+                        if (u >= lo && u < hi) fn(ring[j].v[u]);
+                }
+            }
+            const int nx = ch + D;
+            load_chunk(base + (nx < nch ? nx : nch - 1) * kChunk, ring[j]);
+        }
     }
 }
 
@@ -115,23 +160,14 @@ __device__ __forceinline__ void load_chunk(const double *__restrict__ row, int c
 // ASCENDING i, so after every update positions 1..q-1 all equal the previous errs(0): maTerms is
 // [e_{t-1}, e_{t-2}, e_{t-2}, ...] (a smear for q >= 3, exactly what the reference computes).
 // ------------------------------------------------------------------------------------------------------
-template <int P, int Q, int I>
-struct Model {
-    static constexpr int K = I + P + Q;
-    static constexpr int M = (P > Q ? P : Q);
-};
-
-// One objective step: returns e_t. yl[j] = y_{t-1-j}.
-template <int P, int Q, int I>
-__device__ __forceinline__ double f_step(double yi, const double (&yl)[P > 0 ? P : 1], double e1, double e2,
-                                         double yh0, const double (&c)[I + P + Q > 0 ? I + P + Q : 1]) {
-    double yh = yh0;                                              // 0.0 + intercept * coef(0)   (:600)
-#pragma unroll
-    for (int j = 0; j < P; ++j) yh = yh + yl[j] * c[I + j];       // AR terms, lag 1..p          (:602-605)
-#pragma unroll
-    for (int j = 0; j < Q; ++j) yh = yh + (j == 0 ? e1 : e2) * c[I + P + j];   // MA terms   (:608-611)
-    return yi - yh;                                               // goldStandard(i) - dest(i)  (:613)
-}
+#ifndef STS_PREFETCH_F
+#define STS_PREFETCH_F 4
+#endif
+#ifndef STS_PREFETCH_G
+#define STS_PREFETCH_G 2
+#endif
+constexpr int kPrefetchF = STS_PREFETCH_F;   // chunks in flight per lane in objective passes
+constexpr int kPrefetchG = STS_PREFETCH_G;   // ... in gradient passes (5x the VALU work per byte)
 
 // Full pass. G = false: objective only -> css. G = true: also gradientlogLikelihoodCSSARMA -> g[] (already
 // divided by -sigma2, :532). SMEAR selects the Breeze overlap semantics of :526 (false = row shift).
@@ -143,103 +179,84 @@ __device__ __forceinline__ void css_pass(const double *__restrict__ row, int n,
     constexpr int KA = K > 0 ? K : 1;
     constexpr int M = (P > Q ? P : Q);
     constexpr int PA = P > 0 ? P : 1;
-    double yl[PA];
+    double yl[PA];                        // yl[j] = y_{i-1-j}; the row is padded to >= 16 elements
 #pragma unroll
-    for (int j = 0; j < PA; ++j) yl[j] = 0.0;
+    for (int j = 0; j < PA; ++j) yl[j] = (j < P) ? row[M - 1 - j] : 0.0;
     double e1 = 0.0, e2 = 0.0, css = 0.0, sigma2 = 0.0;
     const double yh0 = 0.0 + (double)I * c[0];
     const double nd = (double)n;
-    double dE[Q + 1][KA];                 // dEdTheta (:476), row r = d e_{t-r} / d theta
+    double dE[G ? Q + 1 : 1][KA];         // dEdTheta (:476), row r = d e_{t-r} / d theta
+    if constexpr (G) {
 #pragma unroll
-    for (int r = 0; r <= Q; ++r)
+        for (int r = 0; r <= Q; ++r)
 #pragma unroll
-        for (int j = 0; j < KA; ++j) dE[r][j] = 0.0;
+            for (int j = 0; j < KA; ++j) dE[r][j] = 0.0;
+    }
 #pragma unroll
     for (int j = 0; j < KA; ++j) g[j] = 0.0;
 
     auto step = [&](double yi) {
         if constexpr (!G) {
-            double e = f_step<P, Q, I>(yi, yl, e1, e2, yh0, c);
-            css = css + e * e;                                    // pow(obs - pred, 2), folded (:440-442)
+            double yh = yh0;                                          // 0.0 + intercept * coef(0)   (:600)
+#pragma unroll
+            for (int j = 0; j < P; ++j) yh = yh + yl[j] * c[I + j];   // AR terms, lag 1..p          (:602-605)
+#pragma unroll
+            for (int j = 0; j < Q; ++j) yh = yh + (j == 0 ? e1 : e2) * c[I + P + j];   // MA terms  (:608-611)
+            const double e = yi - yh;                                 // goldStandard(i) - dest(i)  (:613)
+            css = css + e * e;                                        // pow(obs - pred, 2), folded (:440-442)
             e2 = e1;
             e1 = e;
         } else {
 #pragma unroll
-            for (int j = 0; j < K; ++j)                           // :492-499
+            for (int j = 0; j < K; ++j)                               // :492-499
 #pragma unroll
                 for (int kk = 0; kk < Q; ++kk) dE[0][j] = dE[0][j] - c[I + P + kk] * dE[kk + 1][j];
-            double yh = yh0;                                      // :502
-            if constexpr (K > 0) dE[0][0] = dE[0][0] - (double)I; // :503
+            double yh = yh0;                                          // :502
+            if constexpr (K > 0) dE[0][0] = dE[0][0] - (double)I;     // :503
 #pragma unroll
-            for (int j = 0; j < P; ++j) {                         // :506-510
+            for (int j = 0; j < P; ++j) {                             // :506-510
                 yh = yh + yl[j] * c[I + j];
                 dE[0][I + j] = dE[0][I + j] - yl[j];
             }
 #pragma unroll
-            for (int j = 0; j < Q; ++j) {                         // :514-518
+            for (int j = 0; j < Q; ++j) {                             // :514-518
                 const double mj = (j == 0 ? e1 : e2);
                 yh = yh + mj * c[I + P + j];
                 dE[0][I + P + j] = dE[0][I + P + j] - mj;
             }
-            const double e = yi - yh;                             // :520
+            const double e = yi - yh;                                 // :520
             const double e_sq = e * e;
-            sigma2 = sigma2 + e_sq / nd;                          // :521
-            css = css + e_sq;                                     // objective at the same point (fused)
-            e2 = e1;                                              // :522
+            sigma2 = sigma2 + e_sq / nd;                              // :521
+            css = css + e_sq;                                         // objective at the same point (fused)
+            e2 = e1;                                                  // :522
             e1 = e;
 #pragma unroll
             for (int j = 0; j < K; ++j) g[j] = g[j] + dE[0][j] * e;   // :524
-            if constexpr (SMEAR) {                                // :526, ascending element copy
+            if constexpr (SMEAR) {                                    // :526, ascending element copy
 #pragma unroll
                 for (int r = 1; r <= Q; ++r)
 #pragma unroll
                     for (int j = 0; j < KA; ++j) dE[r][j] = dE[r - 1][j];
-            } else {                                              // :526, memmove-like row shift
+            } else {                                                  // :526, memmove-like row shift
 #pragma unroll
                 for (int r = Q; r >= 1; --r)
 #pragma unroll
                     for (int j = 0; j < KA; ++j) dE[r][j] = dE[r - 1][j];
             }
 #pragma unroll
-            for (int j = 0; j < KA; ++j) dE[0][j] = 0.0;            // :528
+            for (int j = 0; j < KA; ++j) dE[0][j] = 0.0;              // :528
         }
-    };
-    auto shift_lags = [&](double yi) {
         if constexpr (P > 0) {
 #pragma unroll
             for (int j = PA - 1; j >= 1; --j) yl[j] = yl[j - 1];
             yl[0] = yi;
         }
     };
-
-    const int nch = (n + kChunk - 1) / kChunk;
-    Chunk cur, nxt;
-    if (nch > 0) load_chunk(row, 0, cur);
-    for (int ch = 0; ch < nch; ++ch) {
-        if (ch + 1 < nch) load_chunk(row, ch + 1, nxt);
-        const int base = ch * kChunk;
-        if (base >= M && base + kChunk <= n) {                    // interior chunk: no guards
-#pragma unroll
-            for (int u = 0; u < kChunk; ++u) {
-                step(cur.v[u]);
-                shift_lags(cur.v[u]);
-            }
-        } else {
-#pragma unroll
-            for (int u = 0; u < kChunk; ++u) {
-                const int i = base + u;
-                if (i < n) {
-                    if (i >= M) step(cur.v[u]);
-                    shift_lags(cur.v[u]);
-                }
-            }
-        }
-        cur = nxt;
-    }
+    stream_elems<G ? kPrefetchG : kPrefetchF>(row, M, n, step);
     css_out = css;
     if constexpr (G) {
 #pragma unroll
-        for (int j = 0; j < KA; ++j) g[j] = g[j] / -sigma2;     // :532
+        for (int j = 0; j < KA; ++j) g[j] = g[j] / -sigma2;         // :532
     }
 }
 
@@ -251,11 +268,13 @@ __device__ __forceinline__ void css_pass(const double *__restrict__ row, int n,
 // each reflection updates a row independently of the other rows, so every row can be regenerated from the
 // series and re-transformed by the already-known reflections (same ops, same order per element). Two passes
 // per column: (1) xNormSqr -> rDiag[s] = a_s, v_s[s] = x_s[s] - a_s; (2) alpha_{s,c} for c > s and the
-// Q^T y dot product of Solver.solve (which only needs reflection s). The upper triangle of R and the top of
+// Q^T y dot product of Solver.solve (which only needs reflection s). Row s itself (the only row whose v
+// differs) is generated by random access; rows s+1.. are streamed. The upper triangle of R and the top of
 // Q^T y come from re-transforming rows 0..C-1 once more. Back-substitution as Solver.solve.
 //
-// Gen must provide: void row(int r, double (&x)[C], double &y) — the r-th design row (with the intercept
-// column first if any) and response. Rows are requested in increasing r from an arbitrary start.
+// Gen provides: row_at(r, x, y) (random access), begin(r) (prime the sliding window for streaming from row r),
+// first_elem(r) (series index of the element that completes row r), push(v, x, y) (next row from the next
+// series element).
 // ------------------------------------------------------------------------------------------------------
 template <int C>
 struct HouseholderState {
@@ -279,116 +298,182 @@ __device__ __forceinline__ void hh_apply(const HouseholderState<C> &H, int s, do
     }
 }
 
-template <int C, class Gen>
-__device__ int stream_ols(Gen &gen, int R, double (&beta)[C]) {
-    HouseholderState<C> H;
-    double rrow[C][C];    // rrow[i][c] = final qrt[c][i] for c > i (row i of R)
-    double ytop[C];       // final (Q^T y)[i]
-#pragma unroll
-    for (int s = 0; s < C; ++s) {
-        // pass 1: xNormSqr over rows s..R-1 of column s after reflections 0..s-1
-        double xnorm = 0.0, xss = 0.0;
-        for (int r = s; r < R; ++r) {
-            double x[C], y;
-            gen.row(r, x, y);
-            hh_apply<C>(H, s, x, y);
-            if (r == s) xss = x[s];
-            xnorm = xnorm + x[s] * x[s];
+// One Householder stage S (compile-time, so every reflection index below is a constant).
+template <int C, int S, class Gen>
+__device__ __forceinline__ int ols_stage(Gen &gen, const double *__restrict__ row, int n, int R,
+                                         HouseholderState<C> &H) {
+    if constexpr (S == C) {
+        return ARIMA_ST_OK;
+    } else {
+        // pass 1: xNormSqr over rows S..R-1 of column S after reflections 0..S-1
+        double xs[C], ys;
+        gen.row_at(S, xs, ys);
+        hh_apply<C>(H, S, xs, ys);
+        const double xss = xs[S];
+        double xnorm = 0.0 + xss * xss;
+        if (S + 1 < R) {
+            gen.begin(S + 1);
+            stream_elems<2>(row, gen.first_elem(S + 1), n, [&](double v) {
+                double x[C], y;
+                gen.push(v, x, y);
+                hh_apply<C>(H, S, x, y);
+                xnorm = xnorm + x[S] * x[S];
+            });
         }
         const double a = (xss > 0) ? -sqrt(xnorm) : sqrt(xnorm);
-        H.a[s] = a;
+        H.a[S] = a;
         if (a == 0.0) return ARIMA_ST_SINGULAR;   // decompose skips it; Solver.solve then throws Singular
         const double vt = xss - a;
-        H.vtop[s] = vt;
-        // pass 2: alpha_{s,c} (c > s) and the Q^T y dot product, both sequential over rows s..R-1
-        double al[C], dt = 0.0;
+        H.vtop[S] = vt;
+        // pass 2: alpha_{S,c} (c > S) and the Q^T y dot product, both sequential over rows S..R-1
+        double al[C], dt;
 #pragma unroll
-        for (int c = 0; c < C; ++c) al[c] = 0.0;
-        for (int r = s; r < R; ++r) {
-            double x[C], y;
-            gen.row(r, x, y);
-            hh_apply<C>(H, s, x, y);
-            const double v = (r == s) ? vt : x[s];
+        for (int c = 0; c < C; ++c) al[c] = (c > S) ? 0.0 - xs[c] * vt : 0.0;
+        dt = 0.0 + ys * vt;
+        if (S + 1 < R) {
+            gen.begin(S + 1);
+            stream_elems<2>(row, gen.first_elem(S + 1), n, [&](double v) {
+                double x[C], y;
+                gen.push(v, x, y);
+                hh_apply<C>(H, S, x, y);
+                const double vs = x[S];
 #pragma unroll
-            for (int c = s + 1; c < C; ++c) al[c] = al[c] - x[c] * v;
-            dt = dt + y * v;
+                for (int c = S + 1; c < C; ++c) al[c] = al[c] - x[c] * vs;
+                dt = dt + y * vs;
+            });
         }
         const double den = a * vt;
 #pragma unroll
-        for (int c = 0; c < C; ++c) H.alpha[s][c] = (c > s) ? al[c] / den : 0.0;
-        H.dot[s] = dt / den;
+        for (int c = 0; c < C; ++c) H.alpha[S][c] = (c > S) ? al[c] / den : 0.0;
+        H.dot[S] = dt / den;
+        return ols_stage<C, S + 1>(gen, row, n, R, H);
     }
-    // rows 0..C-1 after their own reflection: upper triangle of R and the top of Q^T y
+}
+
+template <int C, class Gen>
+__device__ __forceinline__ int stream_ols(Gen &gen, const double *__restrict__ row, int n, int R, double (&beta)[C]) {
+    HouseholderState<C> H;
+    const int st = ols_stage<C, 0>(gen, row, n, R, H);
+    if (st != ARIMA_ST_OK) return st;
+    // rows 0..C-1 after their own reflection: upper triangle of R (rrow) and the top of Q^T y
+    double rrow[C][C];
+    double ytop[C];
 #pragma unroll
     for (int i = 0; i < C; ++i) {
-        double x[C], y = 0.0;
+        double x[C], y;
+        gen.row_at(i, x, y);
+        hh_apply<C>(H, i, x, y);
+        // reflection i on row i: qrt[c][i] -= alpha * qrt[i][i] (= vtop_i); y[i] += dot * vtop_i
 #pragma unroll
-        for (int c = 0; c < C; ++c) x[c] = 0.0;
-        if (i < R) {
-            gen.row(i, x, y);
-            hh_apply<C>(H, i, x, y);
-            // reflection i on row i: qrt[c][i] -= alpha * qrt[i][i] (= vtop_i); y[i] += dot * vtop_i
-#pragma unroll
-            for (int c = i + 1; c < C; ++c) x[c] = x[c] - H.alpha[i][c] * H.vtop[i];
-            y = y + H.dot[i] * H.vtop[i];
-        }
+        for (int c = i + 1; c < C; ++c) x[c] = x[c] - H.alpha[i][c] * H.vtop[i];
+        y = y + H.dot[i] * H.vtop[i];
 #pragma unroll
         for (int c = 0; c < C; ++c) rrow[i][c] = x[c];
         ytop[i] = y;
     }
     // Solver.solve back-substitution
 #pragma unroll
-    for (int row = C - 1; row >= 0; --row) {
-        ytop[row] = ytop[row] / H.a[row];
-        const double yRow = ytop[row];
-        beta[row] = yRow;
+    for (int r = C - 1; r >= 0; --r) {
+        ytop[r] = ytop[r] / H.a[r];
+        const double yRow = ytop[r];
+        beta[r] = yRow;
 #pragma unroll
         for (int i = 0; i < C; ++i)
-            if (i < row) ytop[i] = ytop[i] - yRow * rrow[i][row];
+            if (i < r) ytop[i] = ytop[i] - yRow * rrow[i][r];
     }
     return ARIMA_ST_OK;
 }
 
 // ------------------------------------------------------------------------------------------------------
 // Row generators over one series (ARIMA.scala:216-242, Autoregression.scala:38-53, Lag.scala:33-99).
-// Plain per-lane loads; rows are walked in order so the lines stay in L1/L2 between rows.
 // ------------------------------------------------------------------------------------------------------
 
 // AR(m) regression: row r = [1?, y(r+m-1), ..., y(r)], response y(r+m).  C = INTERCEPT + m.
+// Streaming: row r is completed by element r + m; window w[l] = y(r + m - l), l = 0..m.
 template <int m, int INTERCEPT>
-struct ARRowGen {
+struct ARGen {
+    static constexpr int C = INTERCEPT + m;
     const double *__restrict__ y;
-    __device__ __forceinline__ void row(int r, double (&x)[INTERCEPT + m], double &yv) const {
+    double w[m + 1];
+    __device__ __forceinline__ void row_at(int r, double (&x)[C], double &yv) const {
         if constexpr (INTERCEPT) x[0] = 1.0;
 #pragma unroll
         for (int l = 1; l <= m; ++l) x[INTERCEPT + l - 1] = y[r + m - l];
         yv = y[r + m];
     }
+    __device__ __forceinline__ int first_elem(int r) const { return r + m; }
+    __device__ __forceinline__ void begin(int r) {
+#pragma unroll
+        for (int l = 1; l <= m; ++l) w[l] = y[r + m - l];
+    }
+    __device__ __forceinline__ void push(double v, double (&x)[C], double &yv) {
+        w[0] = v;
+        if constexpr (INTERCEPT) x[0] = 1.0;
+#pragma unroll
+        for (int l = 1; l <= m; ++l) x[INTERCEPT + l - 1] = w[l];
+        yv = w[0];
+#pragma unroll
+        for (int l = m; l >= 1; --l) w[l] = w[l - 1];
+    }
 };
 
 // Hannan-Rissanen second-stage regression (ARIMA.scala:226-239):
-//   errors(s) = yTrunc(s) - ((sum_j y(s+m-1-j) * a_j) + c)    with yTrunc = y.drop(m)
-//   row r = [1?, yTrunc(r+M-1..r+M-p), errors(r+M-1..r+M-q)],  response yTrunc(r + M)
+//   errors(s) = yTrunc(s) - ((sum_j y(s+m-1-j) * a_j) + c)    with yTrunc = y.drop(m)     (:228-232)
+//   row r = [1?, yTrunc(r+M-1..r+M-p), errors(r+M-1..r+M-q)],  response yTrunc(r + M)   (:234-239)
+// Streaming: row r is completed by element e(r) = m + M + r; y window w[l] = y(e(r) - l), l = 0..m+1;
+// errors window ew[l] = errors(r + M - l), l = 1..q; the newest error of row r is errors(r+M-1), which uses
+// y(e(r)-1-m .. e(r)-1) = w[1..m+1].
 template <int P, int Q, int I>
-struct HRRowGen {
+struct HRGen {
     static constexpr int M = (P > Q ? P : Q);
     static constexpr int m = M + 1;
+    static constexpr int C = I + P + Q;
+    static constexpr int QA = Q > 0 ? Q : 1;
     const double *__restrict__ y;
     double a[m];
     double c;
-    __device__ __forceinline__ double err(int s) const {
+    double w[m + 2];
+    double ew[QA + 1];
+    __device__ __forceinline__ double err_at(int s) const {
         double acc = 0.0;
 #pragma unroll
         for (int j = 0; j < m; ++j) acc = acc + y[s + m - 1 - j] * a[j];
         return y[s + m] - (acc + c);
     }
-    __device__ __forceinline__ void row(int r, double (&x)[I + P + Q > 0 ? I + P + Q : 1], double &yv) const {
+    __device__ __forceinline__ void row_at(int r, double (&x)[C > 0 ? C : 1], double &yv) const {
         if constexpr (I) x[0] = 1.0;
 #pragma unroll
         for (int l = 1; l <= P; ++l) x[I + l - 1] = y[m + r + M - l];
 #pragma unroll
-        for (int l = 1; l <= Q; ++l) x[I + P + l - 1] = err(r + M - l);
+        for (int l = 1; l <= Q; ++l) x[I + P + l - 1] = err_at(r + M - l);
         yv = y[m + r + M];
+    }
+    __device__ __forceinline__ int first_elem(int r) const { return m + M + r; }
+    __device__ __forceinline__ void begin(int r) {
+        const int e = m + M + r;
+#pragma unroll
+        for (int l = 1; l <= m + 1; ++l) w[l] = y[e - l];
+#pragma unroll
+        for (int l = 2; l <= Q; ++l) ew[l] = err_at(r + M - l);
+    }
+    __device__ __forceinline__ void push(double v, double (&x)[C > 0 ? C : 1], double &yv) {
+        w[0] = v;
+        if constexpr (Q > 0) {
+            double acc = 0.0;
+#pragma unroll
+            for (int j = 0; j < m; ++j) acc = acc + w[2 + j] * a[j];
+            ew[1] = w[1] - (acc + c);
+        }
+        if constexpr (I) x[0] = 1.0;
+#pragma unroll
+        for (int l = 1; l <= P; ++l) x[I + l - 1] = w[l];
+#pragma unroll
+        for (int l = 1; l <= Q; ++l) x[I + P + l - 1] = ew[l];
+        yv = w[0];
+#pragma unroll
+        for (int l = m + 1; l >= 1; --l) w[l] = w[l - 1];
+#pragma unroll
+        for (int l = QA; l >= 2; --l) ew[l] = ew[l - 1];
     }
 };
 
@@ -493,11 +578,10 @@ __device__ __forceinline__ bool value_converged(double p, double c, double rel, 
 
 template <int K>
 struct CGLane {
-    // request / response
+    // request / response: xg holds the point to evaluate, then (after a G pass) the gradient
     int req;
-    double x[K];
+    double xg[K];
     double f;
-    double g[K];
     // outcome
     int pc, status;
     int n_eval, n_grad, iter;
@@ -554,7 +638,7 @@ struct CGLane {
                 // r = computeObjectiveGradient(point)
                 req = REQ_G;
 #pragma unroll
-                for (int i = 0; i < K; ++i) x[i] = point[i];
+                for (int i = 0; i < K; ++i) xg[i] = point[i];
                 pc = PC_G0;
                 return;
             case PC_G0: {
@@ -562,8 +646,8 @@ struct CGLane {
                 double dl = 0.0;
 #pragma unroll
                 for (int i = 0; i < K; ++i) {
-                    dir[i] = g[i];                        // steepestDescent = precondition(r) = r.clone()
-                    dl = dl + g[i] * dir[i];
+                    dir[i] = xg[i];                       // steepestDescent = precondition(r) = r.clone()
+                    dl = dl + xg[i] * dir[i];
                 }
                 delta = dl;
                 memo_obj = f;                             // F(point) fused into the gradient pass
@@ -749,12 +833,12 @@ struct CGLane {
                 }
                 if (!pfin) {
 #pragma unroll
-                    for (int i = 0; i < K; ++i) g[i] = __builtin_nan("");
+                    for (int i = 0; i < K; ++i) xg[i] = __builtin_nan("");
                     pc = PC_G;
                     break;
                 }
 #pragma unroll
-                for (int i = 0; i < K; ++i) x[i] = point[i];
+                for (int i = 0; i < K; ++i) xg[i] = point[i];
                 req = REQ_G;
                 pc = PC_G;
                 return;
@@ -764,15 +848,15 @@ struct CGLane {
                 const double deltaOld = delta;
                 double dl = 0.0;
 #pragma unroll
-                for (int i = 0; i < K; ++i) dl = dl + g[i] * g[i];
+                for (int i = 0; i < K; ++i) dl = dl + xg[i] * xg[i];
                 delta = dl;
                 const double beta = delta / deltaOld;       // FLETCHER_REEVES
                 if (iter % K == 0 || beta < 0) {
 #pragma unroll
-                    for (int i = 0; i < K; ++i) dir[i] = g[i];
+                    for (int i = 0; i < K; ++i) dir[i] = xg[i];
                 } else {
 #pragma unroll
-                    for (int i = 0; i < K; ++i) dir[i] = g[i] + beta * dir[i];
+                    for (int i = 0; i < K; ++i) dir[i] = xg[i] + beta * dir[i];
                 }
                 pc = PC_TOP;
                 break;
@@ -788,8 +872,8 @@ struct CGLane {
                 bool fin = true;
 #pragma unroll
                 for (int i = 0; i < K; ++i) {
-                    x[i] = point[i] + ev_alpha * dir[i];
-                    fin = fin && finite(x[i]);
+                    xg[i] = point[i] + ev_alpha * dir[i];
+                    fin = fin && finite(xg[i]);
                 }
                 if (!fin) { ev_val = __builtin_nan(""); pc = ev_ret; break; }
                 req = REQ_F;
@@ -806,6 +890,16 @@ struct CGLane {
             }
         }
     }
+};
+
+// LDS slot of one lane's optimizer state: padded to an odd number of 8-byte words so that 64 lanes reading the
+// same field with ds_read_b64 hit distinct bank pairs (stride = 8 * odd bytes; MI355X_MICROARCH.md LDS table).
+template <int K>
+struct alignas(8) LaneSlot {
+    static constexpr int kWords = (int)((sizeof(CGLane<K>) + 7) / 8);
+    static constexpr int kPadWords = (kWords % 2 == 0) ? 1 : 2;   // total word count odd
+    CGLane<K> s;
+    double pad[kPadWords];
 };
 
 // ------------------------------------------------------------------------------------------------------

@@ -11,34 +11,56 @@ namespace sts {
 constexpr int kMaxD = 16;
 
 // D(i, t) = t < i ? D(i-1, t) : D(i-1, t) - D(i-1, t-1), D(0, t) = ts(t)   (UnivariateTimeSeries.scala:384-480)
+// Evaluated per element from the window ts(t-DD..t) with the same subtractions in the same order.
+template <int DD>
+__device__ __forceinline__ double diff_at(const double *__restrict__ row, int t) {
+    double v[DD + 1];
+#pragma unroll
+    for (int j = 0; j <= DD; ++j) {
+        const int tt = t - DD + j;
+        v[j] = tt >= 0 ? row[tt] : 0.0;
+    }
+#pragma unroll
+    for (int lvl = 1; lvl <= DD; ++lvl)
+#pragma unroll
+        for (int j = DD; j >= lvl; --j)           // position t' = t - DD + j; only j >= lvl is ever needed
+            if (t - DD + j >= lvl) v[j] = v[j] - v[j - 1];
+    return v[DD];
+}
+
+template <int DD>
+__device__ __forceinline__ void diff_rows(const double *__restrict__ in, int64_t ld_in, double *__restrict__ out,
+                                          int64_t ld_out, int64_t N, int T, int drop) {
+    for (int64_t i = blockIdx.x; i < N; i += gridDim.x) {
+        const double *row = in + i * ld_in;
+        double *o = out + i * ld_out;
+        for (int t = (drop ? DD : 0) + (int)threadIdx.x; t < T; t += blockDim.x)
+            o[drop ? t - DD : t] = diff_at<DD>(row, t);
+    }
+}
+
+// one workgroup per row (grid-stride over rows), threads over t: coalesced reads and writes
 __global__ __launch_bounds__(256) void k_difference(const double *__restrict__ in, int64_t ld_in,
                                                     double *__restrict__ out, int64_t ld_out, int64_t N, int T,
                                                     int d, int drop) {
-    const int64_t total = N * (int64_t)T;
-    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-         idx += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = idx / T;
-        const int t = (int)(idx - i * T);
-        if (drop && t < d) continue;
-        const double *row = in + i * ld_in;
-        double v[kMaxD + 1];
-#pragma unroll
-        for (int j = 0; j <= kMaxD; ++j) {
-            const int tt = t - d + j;
-            v[j] = (j <= d && tt >= 0) ? row[tt] : 0.0;
-        }
-        for (int lvl = 1; lvl <= d; ++lvl) {
-            // positions t' = t - d + j, updated only for j >= lvl (higher levels never need lower j)
-            for (int j = d; j >= lvl; --j) {
-                const int tp = t - d + j;
-                if (tp >= lvl) v[j] = v[j] - v[j - 1];
-            }
-        }
-        double r = v[0];
-#pragma unroll
-        for (int j = 0; j <= kMaxD; ++j)
-            if (j == d) r = v[j];
-        out[i * ld_out + (drop ? t - d : t)] = r;
+    switch (d) {
+    case 0: diff_rows<0>(in, ld_in, out, ld_out, N, T, drop); break;
+    case 1: diff_rows<1>(in, ld_in, out, ld_out, N, T, drop); break;
+    case 2: diff_rows<2>(in, ld_in, out, ld_out, N, T, drop); break;
+    case 3: diff_rows<3>(in, ld_in, out, ld_out, N, T, drop); break;
+    case 4: diff_rows<4>(in, ld_in, out, ld_out, N, T, drop); break;
+    case 5: diff_rows<5>(in, ld_in, out, ld_out, N, T, drop); break;
+    case 6: diff_rows<6>(in, ld_in, out, ld_out, N, T, drop); break;
+    case 7: diff_rows<7>(in, ld_in, out, ld_out, N, T, drop); break;
+    case 8: diff_rows<8>(in, ld_in, out, ld_out, N, T, drop); break;
+    case 9: diff_rows<9>(in, ld_in, out, ld_out, N, T, drop); break;
+    case 10: diff_rows<10>(in, ld_in, out, ld_out, N, T, drop); break;
+    case 11: diff_rows<11>(in, ld_in, out, ld_out, N, T, drop); break;
+    case 12: diff_rows<12>(in, ld_in, out, ld_out, N, T, drop); break;
+    case 13: diff_rows<13>(in, ld_in, out, ld_out, N, T, drop); break;
+    case 14: diff_rows<14>(in, ld_in, out, ld_out, N, T, drop); break;
+    case 15: diff_rows<15>(in, ld_in, out, ld_out, N, T, drop); break;
+    default: diff_rows<16>(in, ld_in, out, ld_out, N, T, drop); break;
     }
 }
 
@@ -144,10 +166,8 @@ __global__ __launch_bounds__(256) void k_sample(double *__restrict__ out, int64_
 int launch_difference(const double *in, int64_t ld_in, double *out, int64_t ld_out, int64_t N, int T, int d,
                       int drop, hipStream_t s) {
     if (d > kMaxD) return ARIMA_E_UNSUPPORTED;
-    const int64_t total = N * (int64_t)T;
-    if (total == 0) return ARIMA_OK;
-    const int64_t blocks = (total + 255) / 256;
-    const unsigned grid = (unsigned)(blocks < 65536 * 8 ? blocks : 65536 * 8);
+    if (N == 0 || T == 0) return ARIMA_OK;
+    const unsigned grid = (unsigned)(N < 65536 * 4 ? N : 65536 * 4);
     hipLaunchKernelGGL(k_difference, dim3(grid), dim3(256), 0, s, in, ld_in, out, ld_out, N, T, d, drop);
     STS_CHECK_LAUNCH();
     return ARIMA_OK;
@@ -210,11 +230,11 @@ int launch_ar_fit(const double *y, int64_t ld, int n, int64_t N, int p, int I, d
 int launch_cg_fit(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, int smear,
                   const double *init, const int32_t *init_status, double *coef_out, double *ll_out,
                   int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
-                  unsigned long long *ctl, int grid_blocks, hipStream_t s) {
+                  unsigned long long *ctl, int grid_blocks, int g_permille, hipStream_t s) {
     if (N == 0) return ARIMA_OK;
 #define C_(PP)                                                                                             \
     launch_cg_fit_P<PP>(y, ld, n, N, q, I, smear, init, init_status, coef_out, ll_out, status_out, n_eval_out, \
-                        n_grad_out, flags_out, ctl, grid_blocks, s)
+                        n_grad_out, flags_out, ctl, grid_blocks, g_permille, s)
     STS_P_SWITCH(C_)
 #undef C_
 }

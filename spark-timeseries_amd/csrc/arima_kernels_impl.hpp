@@ -68,17 +68,18 @@ __global__ __launch_bounds__(256) void k_hr_init(const double *__restrict__ y, i
     for (int j = 0; j < KA; ++j) beta[j] = __builtin_nan("");
     if (st == ARIMA_ST_OK) {
         double ab[1 + m];
-        ARRowGen<m, 1> genA{row};
-        st = stream_ols<1 + m>(genA, n - m, ab);                   // Autoregression.fitModel(y, m)  :225
+        ARGen<m, 1> genA;
+        genA.y = row;
+        st = stream_ols<1 + m>(genA, row, n, n - m, ab);           // Autoregression.fitModel(y, m)  :225
         if (st == ARIMA_ST_OK) {
-            HRRowGen<P, Q, I> genB;
+            HRGen<P, Q, I> genB;
             genB.y = row;
             genB.c = ab[0];
 #pragma unroll
             for (int j = 0; j < m; ++j) genB.a[j] = ab[1 + j];
             double bb[KA];
             if constexpr (K > 0) {
-                st = stream_ols<K>(genB, n - m - M, bb);           // :237-240
+                st = stream_ols<K>(genB, row, n, n - m - M, bb);   // :237-240
                 if (st == ARIMA_ST_OK) {
 #pragma unroll
                     for (int j = 0; j < K; ++j) beta[j] = bb[j];
@@ -111,8 +112,9 @@ __global__ __launch_bounds__(256) void k_ar_fit(const double *__restrict__ y, in
     uint8_t fl = 0;
     if (st == ARIMA_ST_OK) {
         double b[K];
-        ARRowGen<P, I> gen{row};
-        st = stream_ols<K>(gen, n - P, b);
+        ARGen<P, I> gen;
+        gen.y = row;
+        st = stream_ols<K>(gen, row, n, n - P, b);
         if (st == ARIMA_ST_OK) {
 #pragma unroll
             for (int j = 0; j < K; ++j) beta[j] = b[j];
@@ -149,23 +151,29 @@ __device__ __forceinline__ void write_fit(int64_t sid, int status, const double 
     if (flags_out) flags_out[sid] = ok ? flags : 0;
 }
 
+// One workgroup of 256 lanes per CU (1 wave per SIMD): every lane's optimizer state lives in LDS
+// (LaneSlot<K>, ~90-150 KB per workgroup), so the registers are free for the pass: its working set plus a
+// kPrefetchF-deep ring of 128-B chunks per lane, which is what keeps HBM busy at this occupancy.
 template <int P, int Q, int I, bool SMEAR>
-__global__ __launch_bounds__(256) void k_cg_fit(const double *__restrict__ y, int64_t ld, int n, int64_t N,
-                                                const double *__restrict__ init,
-                                                const int32_t *__restrict__ init_status,
-                                                double *__restrict__ coef_out, double *__restrict__ ll_out,
-                                                int32_t *__restrict__ status_out, int32_t *__restrict__ n_eval_out,
-                                                int32_t *__restrict__ n_grad_out, uint8_t *__restrict__ flags_out,
-                                                unsigned long long *__restrict__ ctl) {
+__global__ __launch_bounds__(256, 1) void k_cg_fit(const double *__restrict__ y, int64_t ld, int n, int64_t N,
+                                                   const double *__restrict__ init,
+                                                   const int32_t *__restrict__ init_status,
+                                                   double *__restrict__ coef_out, double *__restrict__ ll_out,
+                                                   int32_t *__restrict__ status_out,
+                                                   int32_t *__restrict__ n_eval_out,
+                                                   int32_t *__restrict__ n_grad_out, uint8_t *__restrict__ flags_out,
+                                                   unsigned long long *__restrict__ ctl, int g_permille) {
     // ctl[0] = work counter, ctl[1] = lane F passes, ctl[2] = lane G passes, ctl[3] = wave F-only passes,
     // ctl[4] = wave G passes, ctl[5] = objective evaluations, ctl[6] = gradient evaluations
     constexpr int K = I + P + Q;
-    CGLane<K> L;
+    __shared__ LaneSlot<K> slots[256];
+    CGLane<K> &L = slots[threadIdx.x].s;
     int64_t sid = -1;
     bool idle = false, need_new = true;
     const double *row = y;
     unsigned long long lane_f = 0, lane_g = 0, wave_f = 0, wave_g = 0, evals = 0, grads = 0;
     const bool lane0 = (threadIdx.x & 63) == 0;
+    L.req = REQ_NONE;
     for (;;) {
         // ---- per lane: advance the state machine to its next request (refilling finished lanes) ----
         while (!idle) {
@@ -189,11 +197,15 @@ __global__ __launch_bounds__(256) void k_cg_fit(const double *__restrict__ y, in
                 for (int j = 0; j < K; ++j) x0[j] = init[sid * K + j];
                 L.start(x0);
             }
+            if (L.req != REQ_NONE) break;        // request still pending (deferred G): nothing to advance
             L.advance();
             if (L.done()) {
-                write_fit<K>(sid, L.status, L.point, L.prev_obj, L.n_eval, L.n_grad,
-                             L.status == ARIMA_ST_OK ? model_flags<P, Q, I>(L.point) : (uint8_t)0, coef_out,
-                             ll_out, status_out, n_eval_out, n_grad_out, flags_out);
+                double pt[K];
+#pragma unroll
+                for (int j = 0; j < K; ++j) pt[j] = L.point[j];
+                write_fit<K>(sid, L.status, pt, L.prev_obj, L.n_eval, L.n_grad,
+                             L.status == ARIMA_ST_OK ? model_flags<P, Q, I>(pt) : (uint8_t)0, coef_out, ll_out,
+                             status_out, n_eval_out, n_grad_out, flags_out);
                 evals += L.n_eval;
                 grads += L.n_grad;
                 need_new = true;
@@ -201,22 +213,33 @@ __global__ __launch_bounds__(256) void k_cg_fit(const double *__restrict__ y, in
             }
             break;
         }
-        // ---- per wave: one pass serving every posted request ----
-        if (__ballot(!idle) == 0ull) break;
-        const bool anyG = __ballot(!idle && L.req == REQ_G) != 0ull;
-        double css, g[K];
+        // ---- per wave: one pass serving the posted requests ----
+        const unsigned long long act = __ballot(!idle);
+        if (act == 0ull) break;
+        // G-pass policy: a gradient pass costs several objective passes; lanes waiting for G sit out F-only
+        // passes until at least g_permille/1000 of the active lanes want G (or nobody wants F).
+        const int req = idle ? REQ_NONE : L.req;
+        const unsigned long long wantG = __ballot(req == REQ_G);
+        const int nG = __popcll(wantG), nA = __popcll(act);
+        const bool anyG = nG > 0 && (nG == nA || nG * 1000 >= g_permille * nA);
+        // lanes not served by this pass stream a shared row (L2-resident) instead of their own
+        const bool served = !idle && (anyG || req == REQ_F);
+        const double *prow = served ? row : y;
+        double c[K], css, g[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) c[j] = served ? L.xg[j] : 0.0;
         if (anyG) {
-            css_pass<P, Q, I, true, SMEAR>(row, n, L.x, css, g);
+            css_pass<P, Q, I, true, SMEAR>(prow, n, c, css, g);
             wave_g += lane0;
         } else {
-            css_pass<P, Q, I, false, SMEAR>(row, n, L.x, css, g);
+            css_pass<P, Q, I, false, SMEAR>(prow, n, c, css, g);
             wave_f += lane0;
         }
-        if (!idle) {
+        if (served) {
             L.f = css_to_loglik(css, n);
-            if (L.req == REQ_G) {
+            if (req == REQ_G) {
 #pragma unroll
-                for (int j = 0; j < K; ++j) L.g[j] = g[j];
+                for (int j = 0; j < K; ++j) L.xg[j] = g[j];
                 lane_g++;
             } else {
                 lane_f++;
@@ -346,7 +369,7 @@ template <int P>
 int launch_cg_fit_P(const double *y, int64_t ld, int n, int64_t N, int q, int I, int smear, const double *init,
                     const int32_t *init_status, double *coef_out, double *ll_out, int32_t *status_out,
                     int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out, unsigned long long *ctl,
-                    int grid_blocks, hipStream_t s) {
+                    int grid_blocks, int g_permille, hipStream_t s) {
     return with_order(q, [&](auto Qc) {
         return with_bool(I, [&](auto Ic) {
             return with_bool(smear, [&](auto Sc) {
@@ -357,7 +380,7 @@ int launch_cg_fit_P(const double *y, int64_t ld, int n, int64_t N, int q, int I,
                 } else {
                     hipLaunchKernelGGL((k_cg_fit<P, Q, II, S>), dim3(grid_blocks), dim3(256), 0, s, y, ld, n, N, init,
                                        init_status, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out,
-                                       ctl);
+                                       ctl, g_permille);
                     STS_CHECK_LAUNCH();
                     return ARIMA_OK;
                 }
@@ -434,7 +457,7 @@ int launch_model_flags_P(const double *coef, int64_t N, int q, int I, uint8_t *f
                                          int32_t *, int32_t *, int32_t *, uint8_t *, hipStream_t);              \
     EXT template int launch_cg_fit_P<PP>(const double *, int64_t, int, int64_t, int, int, int, const double *,   \
                                          const int32_t *, double *, double *, int32_t *, int32_t *, int32_t *,  \
-                                         uint8_t *, unsigned long long *, int, hipStream_t);                     \
+                                         uint8_t *, unsigned long long *, int, int, hipStream_t);                \
     EXT template int cg_fit_occupancy_blocks_P<PP>(int, int, int);                                              \
     EXT template int launch_css_loglik_P<PP>(const double *, int64_t, int, int64_t, int, int, const double *,    \
                                              double *, hipStream_t);                                            \

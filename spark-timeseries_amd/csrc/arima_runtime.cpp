@@ -55,6 +55,8 @@ struct arima_handle {
     arima_fit_stats stats{};
     int smear = 0;
     int grid_blocks_override = 0;
+    int g_permille = 0;
+    int64_t last_grid = 0;
     // device workspaces
     DevBuf diff, init, hr_status, ctl;
     // host-API staging
@@ -179,6 +181,7 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
     if (!h || !name) return ARIMA_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
     if (!strcmp(name, "smear")) { h->smear = value ? 1 : 0; return ARIMA_OK; }
+    if (!strcmp(name, "g_permille")) { h->g_permille = (int)std::min<int64_t>(1000, std::max<int64_t>(0, value)); return ARIMA_OK; }
     if (!strcmp(name, "grid_blocks")) { h->grid_blocks_override = (int)std::max<int64_t>(0, value); return ARIMA_OK; }
     return set_err(h, ARIMA_E_INVALID_ARG, "unknown option");
 }
@@ -240,8 +243,10 @@ static int fit_device_locked(arima_handle *h, const double *d_series, int64_t N,
             }
             const int64_t need = (N + 255) / 256;
             if (blocks > need) blocks = (int)need;
+            h->last_grid = blocks;
             RCCHK(h, sts::launch_cg_fit(y, ldn, n, N, p, q, I, h->smear, init, init_status, d_coef, d_ll, d_status,
-                                        d_neval, d_ngrad, d_flags, h->ctl.as<unsigned long long>(), blocks, s),
+                                        d_neval, d_ngrad, d_flags, h->ctl.as<unsigned long long>(), blocks,
+                                        h->g_permille, s),
                   "cg_fit");
         }
         HIPCHK(h, hipEventRecord(h->ev[3], s));
@@ -262,6 +267,9 @@ static int fit_device_locked(arima_handle *h, const double *d_series, int64_t N,
     st.g_passes = (int64_t)c[2];
     st.n_eval = (int64_t)c[5];
     st.n_grad = (int64_t)c[6];
+    st.wave_f_passes = (int64_t)c[3];
+    st.wave_g_passes = (int64_t)c[4];
+    st.grid_blocks = h->last_grid;
     // HR passes: 2 per column of each of the two least squares (+1 re-transform sweep over C rows)
     const int M = std::max(p, q), m = M + 1;
     if (p > 0 && q == 0) st.hr_passes = N * (int64_t)(2 * (I + p));
