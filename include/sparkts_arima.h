@@ -77,6 +77,8 @@ typedef struct arima_fit_stats {
     int64_t wave_f_passes;   /* wave-level objective-only passes of the fit kernel                   */
     int64_t wave_g_passes;   /* wave-level passes that included the gradient recursion               */
     int64_t grid_blocks;     /* workgroups of the persistent fit kernel                               */
+    int64_t spec_hits;       /* objective evaluations answered by a speculative line-search point     */
+    int64_t wave_multi_passes; /* wave-level objective passes that carried speculative points          */
 } arima_fit_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------------------- */

@@ -337,7 +337,20 @@ typedef struct {
     const double *y;
     int n, p, q, I, k, smear;
     int n_eval, n_grad, n_iter;
+    /* optional evaluation trace (analysis only): phase (0 top, 1 bracket, 2 brent, 3 gradient), alpha */
+    int *tr_phase;
+    double *tr_alpha;
+    int tr_len, tr_cap, tr_cur_phase;
+    double tr_cur_alpha;
 } orc_ctx;
+
+static void trace(orc_ctx *c, int phase, double alpha) {
+    if (c->tr_phase && c->tr_len < c->tr_cap) {
+        c->tr_phase[c->tr_len] = phase;
+        c->tr_alpha[c->tr_len] = alpha;
+        c->tr_len++;
+    }
+}
 
 /* BaseOptimizer.computeObjectiveValue: evaluations.incrementCount() (throws past MaxEval) then f */
 static int cg_obj(orc_ctx *c, const double *x, double *f) {
@@ -350,6 +363,7 @@ static int cg_obj(orc_ctx *c, const double *x, double *f) {
 /* LineSearch.search's univariate function: x[i] = startPoint[i] + alpha * direction[i] */
 static int ls_f(orc_ctx *c, const double *start, const double *dir, double alpha, double *f) {
     double x[ORC_KMAX];
+    trace(c, c->tr_cur_phase, alpha);
     for (int i = 0; i < c->k; i++) x[i] = start[i] + alpha * dir[i];
     return cg_obj(c, x, f);
 }
@@ -358,7 +372,10 @@ static int ls_f(orc_ctx *c, const double *start, const double *dir, double alpha
 static int br_eval(orc_ctx *c, int *bcount, const double *start, const double *dir, double alpha, double *f) {
     if (*bcount + 1 > ORC_BRACKET_MAX) return ARIMA_ST_BRACKET_MAX_EVAL;
     (*bcount)++;
-    return ls_f(c, start, dir, alpha, f);
+    c->tr_cur_phase = 1;
+    int st = ls_f(c, start, dir, alpha, f);
+    c->tr_cur_phase = 2;
+    return st;
 }
 
 /* Precision.equals(x, y) with maxUlps = 1 */
@@ -521,6 +538,7 @@ static int line_search(orc_ctx *c, const double *start, const double *dir, doubl
 /* gradient function call (not counted as an evaluation) */
 static void cg_grad(orc_ctx *c, const double *x, double *g) {
     c->n_grad++;
+    trace(c, 3, 0.0);
     orc_gradient_css_arma(c->y, c->n, c->p, c->q, c->I, x, c->smear, g);
 }
 
@@ -540,6 +558,7 @@ static int cg_optimize(orc_ctx *c, const double *init, double *point_out, double
         if (c->n_iter + 1 > ORC_MAX_ITER) return ARIMA_ST_MAX_ITER;
         c->n_iter++;
         double objective;
+        trace(c, 0, 0.0);
         if ((st = cg_obj(c, point, &objective))) return st;
         int converged = have_cur && value_converged(cur_obj, objective, 1e-7, 1e-7);
         cur_obj = objective; have_cur = 1;
@@ -602,7 +621,7 @@ int orc_fit(const double *ts, int T, int p, int d, int q, int I, int method, con
     }
     if (method != ARIMA_METHOD_CSS_CGD) { free(tmp); return ARIMA_ST_UNSUPPORTED_METHOD; }  /* :105-109 */
     if (k == 0) { free(tmp); return ARIMA_ST_ZERO_PARAMS; }
-    orc_ctx c = {y, n, p, q, I, k, smear, 0, 0, 0};
+    orc_ctx c = {y, n, p, q, I, k, smear, 0, 0, 0, NULL, NULL, 0, 0, 2, 0.0};
     double pt[ORC_KMAX], obj;
     st = cg_optimize(&c, init, pt, &obj);                         /* :174-200 */
     counters[0] = c.n_eval; counters[1] = c.n_grad; counters[2] = c.n_iter;
@@ -610,6 +629,25 @@ int orc_fit(const double *ts, int T, int p, int d, int q, int I, int method, con
         memcpy(coef_out, pt, sizeof(double) * (size_t)k);
         *ll_out = obj;
     }
+    free(tmp);
+    return st;
+}
+
+/* Same as orc_fit (CG path only, user_init or HR init) with an evaluation trace (analysis tool). */
+int orc_fit_trace(const double *ts, int T, int p, int d, int q, int I, int smear, int *tr_phase,
+                  double *tr_alpha, int tr_cap, int *tr_len) {
+    int k = I + p + q;
+    double *tmp = (double *)malloc(sizeof(double) * (size_t)(T > 0 ? T : 1));
+    orc_differences_of_order_d(ts, T, d, tmp);
+    int n = T - d;
+    const double *y = tmp + d;
+    double init[ORC_KMAX];
+    int st = orc_hannan_rissanen(y, n, p, q, I, init);
+    if (st) { free(tmp); *tr_len = 0; return st; }
+    orc_ctx c = {y, n, p, q, I, k, smear, 0, 0, 0, tr_phase, tr_alpha, 0, tr_cap, 2, 0.0};
+    double pt[ORC_KMAX], obj;
+    st = cg_optimize(&c, init, pt, &obj);
+    *tr_len = c.tr_len;
     free(tmp);
     return st;
 }

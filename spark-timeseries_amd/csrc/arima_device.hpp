@@ -260,6 +260,47 @@ __device__ __forceinline__ void css_pass(const double *__restrict__ row, int n,
     }
 }
 
+// Objective pass for NCH points at once (speculative line-search points): NCH independent recursions over the
+// same streamed series. Each chain is exactly the single-point objective (same ops, same order).
+template <int P, int Q, int I, int NCH>
+__device__ __forceinline__ void css_pass_multi(const double *__restrict__ row, int n,
+                                               const double (&c)[NCH][I + P + Q > 0 ? I + P + Q : 1],
+                                               double (&css_out)[NCH]) {
+    constexpr int M = (P > Q ? P : Q);
+    constexpr int PA = P > 0 ? P : 1;
+    double yl[PA];
+#pragma unroll
+    for (int j = 0; j < PA; ++j) yl[j] = (j < P) ? row[M - 1 - j] : 0.0;
+    double e1[NCH], e2[NCH], css[NCH], yh0[NCH];
+#pragma unroll
+    for (int h = 0; h < NCH; ++h) {
+        e1[h] = e2[h] = css[h] = 0.0;
+        yh0[h] = 0.0 + (double)I * c[h][0];
+    }
+    auto step = [&](double yi) {
+#pragma unroll
+        for (int h = 0; h < NCH; ++h) {
+            double yh = yh0[h];
+#pragma unroll
+            for (int j = 0; j < P; ++j) yh = yh + yl[j] * c[h][I + j];
+#pragma unroll
+            for (int j = 0; j < Q; ++j) yh = yh + (j == 0 ? e1[h] : e2[h]) * c[h][I + P + j];
+            const double e = yi - yh;
+            css[h] = css[h] + e * e;
+            e2[h] = e1[h];
+            e1[h] = e;
+        }
+        if constexpr (P > 0) {
+#pragma unroll
+            for (int j = PA - 1; j >= 1; --j) yl[j] = yl[j - 1];
+            yl[0] = yi;
+        }
+    };
+    stream_elems<kPrefetchF>(row, M, n, step);
+#pragma unroll
+    for (int h = 0; h < NCH; ++h) css_out[h] = css[h];
+}
+
 // ------------------------------------------------------------------------------------------------------
 // Streaming Householder least squares, bit-identical to commons-math3 3.4.1
 // OLSMultipleLinearRegression + QRDecomposition(threshold 0) without materialising the design matrix.
@@ -542,6 +583,19 @@ __device__ __forceinline__ uint8_t model_flags(const double (&c)[I + P + Q > 0 ?
 // ------------------------------------------------------------------------------------------------------
 enum : int { REQ_NONE = 0, REQ_F = 1, REQ_G = 2 };
 
+// Speculative line-search points. In most line searches the bracket's next points do not depend on function
+// values (BracketFinder's golden extension xC = xB + GOLD(xB - xA), then the grow-limit extrapolation
+// wLim = xB + 100 (xC - xB) while the objective keeps rising), so an objective request in the bracket phase
+// carries up to kSpec predicted alphas. The pass evaluates them as extra chains over the same streamed series
+// (same bytes); their values go into a per-lane cache keyed by the exact alpha bits, consulted before any
+// later evaluation of the same line search. A hit is a point the reference evaluates with the same operations,
+// so results (and evaluation counts) are unchanged; a miss only costs the extra chain's arithmetic.
+#ifndef STS_SPEC
+#define STS_SPEC 3
+#endif
+template <int K>
+constexpr int spec_slots() { return K <= 8 ? STS_SPEC : 0; }   // LDS budget: no speculation at K > 8
+
 enum : int {
     PC_START = 0, PC_G0, PC_TOP, PC_BR_FA, PC_BR_FB, PC_BR_FC, PC_BR_LOOP, PC_BR_A1, PC_BR_C1,
     PC_BR_SHIFT_EV, PC_BR_SHIFT, PC_BR_END, PC_BRENT_FX, PC_BRENT_LOOP, PC_BRENT_FU, PC_LS_DONE, PC_G,
@@ -599,6 +653,11 @@ struct CGLane {
     // eval subroutine
     double ev_alpha, ev_memo, ev_val;
     int ev_memo_ok, ev_bracket, ev_ret;
+    // speculation: cache of the current line search, and the predicted alphas of the posted request
+    static constexpr int NS = spec_slots<K>();
+    static constexpr int NS1 = NS > 0 ? NS : 1;
+    double sp_alpha[NS1], sp_f[NS1], rq_spec[NS1];
+    int sp_n, rq_nspec, spec_hits;
 
     __device__ __forceinline__ void start(const double (&init)[K]) {
 #pragma unroll
@@ -608,6 +667,7 @@ struct CGLane {
         n_eval = n_grad = iter = 0;
         have_prev_obj = 0;
         req = REQ_NONE;
+        sp_n = rq_nspec = spec_hits = 0;
     }
 
     __device__ __forceinline__ void fail(int st) {
@@ -665,6 +725,7 @@ struct CGLane {
                 have_prev_obj = 1;
                 if (conv) { pc = PC_DONE; return; }   // status OK; point / prev_obj are the result
                 // line.search(point, searchDirection)
+                sp_n = 0;
                 bcount = 0;
                 xA = 0.0;
                 xB = 1e-8;
@@ -876,6 +937,41 @@ struct CGLane {
                     fin = fin && finite(xg[i]);
                 }
                 if (!fin) { ev_val = __builtin_nan(""); pc = ev_ret; break; }
+                rq_nspec = 0;
+                if constexpr (NS > 0) {
+                    const long long ab = __double_as_longlong(ev_alpha);
+                    bool hit = false;
+                    for (int s = 0; s < sp_n; ++s)
+                        if (__double_as_longlong(sp_alpha[s]) == ab) { ev_val = sp_f[s]; hit = true; }
+                    if (hit) { spec_hits++; pc = ev_ret; break; }
+                    // predict the bracket's next value-independent points (same expressions as below)
+                    double bb = 0.0, cc = 0.0;
+                    bool chain = true;
+                    switch (ev_ret) {
+                    case PC_BR_FB:                                      // xC if fA <= fB, then the wLim chain
+                        cc = xB + GOLD * (xB - xA);
+                        rq_spec[rq_nspec++] = cc;
+                        bb = xB;
+                        break;
+                    case PC_BR_FC: bb = xB; cc = xC; break;            // wLim chain from (xB, xC)
+                    case PC_BR_SHIFT_EV: bb = xC; cc = w; break;       // the shift makes (xB, xC) = (xC, w)
+                    case PC_BR_A1:                                      // no break: golden extension
+                        rq_spec[rq_nspec++] = xC + GOLD * (xC - xB);
+                        chain = false;
+                        break;
+                    case PC_BR_C1:                                      // fW > fC: golden extension from w
+                        rq_spec[rq_nspec++] = w + GOLD * (w - xC);
+                        chain = false;
+                        break;
+                    default: chain = false; break;
+                    }
+                    while (chain && rq_nspec < NS) {
+                        const double nx = bb + GROW * (cc - bb);
+                        rq_spec[rq_nspec++] = nx;
+                        bb = cc;
+                        cc = nx;
+                    }
+                }
                 req = REQ_F;
                 pc = PC_EVAL_RESP;
                 return;

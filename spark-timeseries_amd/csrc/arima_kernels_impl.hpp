@@ -171,7 +171,7 @@ __global__ __launch_bounds__(256, 1) void k_cg_fit(const double *__restrict__ y,
     int64_t sid = -1;
     bool idle = false, need_new = true;
     const double *row = y;
-    unsigned long long lane_f = 0, lane_g = 0, wave_f = 0, wave_g = 0, evals = 0, grads = 0;
+    unsigned long long lane_f = 0, lane_g = 0, wave_f = 0, wave_g = 0, wave_m = 0, evals = 0, grads = 0, hits = 0;
     const bool lane0 = (threadIdx.x & 63) == 0;
     L.req = REQ_NONE;
     for (;;) {
@@ -208,6 +208,7 @@ __global__ __launch_bounds__(256, 1) void k_cg_fit(const double *__restrict__ y,
                              status_out, n_eval_out, n_grad_out, flags_out);
                 evals += L.n_eval;
                 grads += L.n_grad;
+                hits += L.spec_hits;
                 need_new = true;
                 continue;
             }
@@ -228,9 +229,37 @@ __global__ __launch_bounds__(256, 1) void k_cg_fit(const double *__restrict__ y,
         double c[K], css, g[K];
 #pragma unroll
         for (int j = 0; j < K; ++j) c[j] = served ? L.xg[j] : 0.0;
+        constexpr int NS = CGLane<K>::NS;
+        const int nspec = (served && req == REQ_F) ? L.rq_nspec : 0;
+        const bool anySpec = NS > 0 && !anyG && __ballot(nspec > 0) != 0ull;
         if (anyG) {
             css_pass<P, Q, I, true, SMEAR>(prow, n, c, css, g);
             wave_g += lane0;
+        } else if constexpr (NS > 0) {
+            if (anySpec) {
+                // primary point + the lane's speculative points (lanes with fewer repeat the primary)
+                double cm[NS + 1][K], cssm[NS + 1];
+#pragma unroll
+                for (int j = 0; j < K; ++j) cm[0][j] = c[j];
+#pragma unroll
+                for (int h = 0; h < NS; ++h) {
+                    const bool use = h < nspec;
+                    const double al = use ? L.rq_spec[h] : 0.0;
+#pragma unroll
+                    for (int j = 0; j < K; ++j) cm[h + 1][j] = use ? L.point[j] + al * L.dir[j] : c[j];
+                }
+                css_pass_multi<P, Q, I, NS + 1>(prow, n, cm, cssm);
+                css = cssm[0];
+                for (int h = 0; h < nspec; ++h) {
+                    L.sp_alpha[h] = L.rq_spec[h];
+                    L.sp_f[h] = css_to_loglik(cssm[h + 1], n);
+                }
+                if (nspec > 0) L.sp_n = nspec;
+                wave_m += lane0;
+            } else {
+                css_pass<P, Q, I, false, SMEAR>(prow, n, c, css, g);
+                wave_f += lane0;
+            }
         } else {
             css_pass<P, Q, I, false, SMEAR>(prow, n, c, css, g);
             wave_f += lane0;
@@ -255,6 +284,8 @@ __global__ __launch_bounds__(256, 1) void k_cg_fit(const double *__restrict__ y,
     }
     atomicAdd(&ctl[5], evals);
     atomicAdd(&ctl[6], grads);
+    atomicAdd(&ctl[7], hits);
+    if (lane0) atomicAdd(&ctl[8], wave_m);
 }
 
 // =======================================================================================================

@@ -55,7 +55,7 @@ struct arima_handle {
     arima_fit_stats stats{};
     int smear = 0;
     int grid_blocks_override = 0;
-    int g_permille = 0;
+    int g_permille = 750;     // G-pass deferral (see k_cg_fit); tuned on C2
     int64_t last_grid = 0;
     // device workspaces
     DevBuf diff, init, hr_status, ctl;
@@ -269,6 +269,8 @@ static int fit_device_locked(arima_handle *h, const double *d_series, int64_t N,
     st.n_grad = (int64_t)c[6];
     st.wave_f_passes = (int64_t)c[3];
     st.wave_g_passes = (int64_t)c[4];
+    st.spec_hits = (int64_t)c[7];
+    st.wave_multi_passes = (int64_t)c[8];
     st.grid_blocks = h->last_grid;
     // HR passes: 2 per column of each of the two least squares (+1 re-transform sweep over C rows)
     const int M = std::max(p, q), m = M + 1;

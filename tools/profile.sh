@@ -1,0 +1,20 @@
+#!/bin/bash
+# Profile the headline bench with rocprofv3 (run ON the GPU box, from the repo root):
+#   1) kernel trace + stats  -> gpurun_out/prof_trace/...  (per-kernel average durations)
+#   2) PMC pass: FETCH_SIZE, WRITE_SIZE (HBM traffic) -> gpurun_out/prof_pmc/...
+#   3) PMC pass: SQ counters (VALU / waves / wait) -> gpurun_out/prof_sq/...
+# Counters are collected in their own runs with --kernel-trace only (no sys/runtime trace), per the guide.
+set -euo pipefail
+cd /tmp && export TMPDIR=/tmp
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+SER=${SER:-1048576}
+OUT=gpurun_out
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_trace -o run --output-format csv -- \
+    python3 bench.py --series $SER --steps 2 --warmup 1 --cpu-seconds 0 > $OUT/prof_bench.json 2> $OUT/prof_bench.err
+timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/prof_fetch -o run --output-format csv -- \
+    python3 bench.py --series $SER --steps 1 --warmup 0 --cpu-seconds 0 > /dev/null 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/prof_write -o run --output-format csv -- \
+    python3 bench.py --series $SER --steps 1 --warmup 0 --cpu-seconds 0 > /dev/null 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d $OUT/prof_sq -o run --output-format csv -- \
+    python3 bench.py --series $SER --steps 1 --warmup 0 --cpu-seconds 0 > /dev/null 2>&1
+find $OUT/prof_* -name "*.csv" | head -50
