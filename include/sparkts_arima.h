@@ -79,6 +79,9 @@ typedef struct arima_fit_stats {
     int64_t grid_blocks;     /* workgroups of the persistent fit kernel                               */
     int64_t spec_hits;       /* objective evaluations answered by a speculative line-search point     */
     int64_t wave_multi_passes; /* wave-level objective passes that carried speculative points          */
+    int64_t diag[6];         /* diagnostics of builds with -DSTS_TIMING (shader cycles summed over waves:
+                                [0] optimizer state machine, [1] all passes, [2] wave lifetime,
+                                [3] gradient passes, [4] multi-point passes); else 0                  */
 } arima_fit_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------------------- */

@@ -591,7 +591,7 @@ enum : int { REQ_NONE = 0, REQ_F = 1, REQ_G = 2 };
 // later evaluation of the same line search. A hit is a point the reference evaluates with the same operations,
 // so results (and evaluation counts) are unchanged; a miss only costs the extra chain's arithmetic.
 #ifndef STS_SPEC
-#define STS_SPEC 3
+#define STS_SPEC 1
 #endif
 template <int K>
 constexpr int spec_slots() { return K <= 8 ? STS_SPEC : 0; }   // LDS budget: no speculation at K > 8
@@ -599,7 +599,7 @@ constexpr int spec_slots() { return K <= 8 ? STS_SPEC : 0; }   // LDS budget: no
 enum : int {
     PC_START = 0, PC_G0, PC_TOP, PC_BR_FA, PC_BR_FB, PC_BR_FC, PC_BR_LOOP, PC_BR_A1, PC_BR_C1,
     PC_BR_SHIFT_EV, PC_BR_SHIFT, PC_BR_END, PC_BRENT_FX, PC_BRENT_LOOP, PC_BRENT_FU, PC_LS_DONE, PC_G,
-    PC_EVAL, PC_EVAL_RESP, PC_DONE
+    PC_EVAL, PC_DONE
 };
 
 // Precision.equals(x, y, 1)
@@ -630,34 +630,27 @@ __device__ __forceinline__ bool value_converged(double p, double c, double rel, 
     return (diff <= size * rel) || (diff <= abs_);
 }
 
-template <int K>
+// One lane's optimizer state, kept compact because it lives in LDS for every lane of the persistent fit kernel
+// and its size sets how many waves share a CU: bracket and Brent fields share storage (they are
+// never live together), the request point is recomputed by the pass from (point, dir, ev_alpha) with the same
+// operations, responses arrive as advance() arguments (registers), counters are 16-bit (all bounded by 10001).
+template <int K, int NS_>
 struct CGLane {
-    // request / response: xg holds the point to evaluate, then (after a G pass) the gradient
-    int req;
-    double xg[K];
-    double f;
-    // outcome
-    int pc, status;
-    int n_eval, n_grad, iter;
-    // optimizer
+    static constexpr int NS = NS_;
+    static constexpr int NS1 = NS > 0 ? NS : 1;
+    // optimizer (NonLinearConjugateGradientOptimizer.doOptimize)
     double point[K], dir[K];
     double delta, memo_obj, prev_obj;
-    int have_prev_obj;
-    // bracket
-    int bcount;
-    double xA, xB, xC, fA, fB, fC, w, fW;
-    // brent
-    double a, b, bx, bv, bw, bd, be, fx, fv, fw, u;
-    double prev_x, prev_f, cur_x, cur_f, best_x, best_f;
-    int have_prev;
-    // eval subroutine
-    double ev_alpha, ev_memo, ev_val;
-    int ev_memo_ok, ev_bracket, ev_ret;
+    // line search: BracketFinder and BrentOptimizer state (disjoint lifetimes)
+    union {
+        struct { double xA, xB, xC, fA, fB, fC, w, fW; };
+        struct { double a, b, bx, bv, bw, bd, be, fx, fv, fw, u, prev_x, prev_f, cur_x, cur_f, best_x, best_f; };
+    };
+    double ev_alpha;                       // pending objective request: point + ev_alpha * dir
     // speculation: cache of the current line search, and the predicted alphas of the posted request
-    static constexpr int NS = spec_slots<K>();
-    static constexpr int NS1 = NS > 0 ? NS : 1;
     double sp_alpha[NS1], sp_f[NS1], rq_spec[NS1];
-    int sp_n, rq_nspec, spec_hits;
+    uint16_t n_eval, n_grad, iter, bcount, spec_hits;
+    uint8_t pc, status, req, have_prev_obj, have_prev, sp_n, rq_nspec;
 
     __device__ __forceinline__ void start(const double (&init)[K]) {
 #pragma unroll
@@ -667,38 +660,53 @@ struct CGLane {
         n_eval = n_grad = iter = 0;
         have_prev_obj = 0;
         req = REQ_NONE;
-        sp_n = rq_nspec = spec_hits = 0;
+        sp_n = rq_nspec = 0;
+        spec_hits = 0;
     }
 
     __device__ __forceinline__ void fail(int st) {
-        status = st;
+        status = (uint8_t)st;
         pc = PC_DONE;
     }
 
     __device__ __forceinline__ bool done() const { return pc == PC_DONE; }
 
-    // schedule an objective evaluation of point + alpha*dir, resuming at `ret` with ev_val set
-    __device__ __forceinline__ void eval(double alpha, int bracket, int memo_ok, double memo, int ret) {
-        ev_alpha = alpha;
-        ev_bracket = bracket;
-        ev_memo_ok = memo_ok;
-        ev_memo = memo;
-        ev_ret = ret;
-        pc = PC_EVAL;
+    // coefficients of the posted request (the same expression PC_EVAL checks for finiteness)
+    __device__ __forceinline__ void request_point(double (&c)[K]) const {
+        if (req == REQ_G) {
+#pragma unroll
+            for (int i = 0; i < K; ++i) c[i] = point[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < K; ++i) c[i] = point[i] + ev_alpha * dir[i];
+        }
     }
 
-    // Run the state machine until a request is posted (req != REQ_NONE) or the fit is finished.
-    // On entry with req == REQ_NONE after a served request, f (and g for REQ_G) hold the response.
-    __device__ void advance() {
+    // Run the state machine until a request is posted (req != REQ_NONE) or the fit is finished. fr / gr are
+    // the response to the request served last (objective; and the gradient for a G request).
+    __device__ void advance(double fr, const double (&gr)[K]) {
         const double GOLD = 1.618034, EPS_MIN = 1e-21, GROW = 100.0;
         const double GS = 0.5 * (3 - __builtin_sqrt(5.0));   // BrentOptimizer.GOLDEN_SECTION
+        double ev_val = fr;                                   // objective value delivered to the resume point
+        double grad[K];                                       // gradient delivered to PC_G0 / PC_G
+#pragma unroll
+        for (int i = 0; i < K; ++i) grad[i] = gr[i];
+        // eval subroutine (LineSearch's objective): locals of this call, never live across a pass
+        double ev_memo = 0.0;
+        int ev_memo_ok = 0, ev_bracket = 0, ev_ret = PC_DONE;
+        auto eval = [&](double alpha, int bracket, int memo_ok, double memo, int ret) {
+            ev_alpha = alpha;
+            ev_bracket = bracket;
+            ev_memo_ok = memo_ok;
+            ev_memo = memo;
+            ev_ret = ret;
+            pc = PC_EVAL;
+        };
         for (;;) {
             switch (pc) {
             case PC_START:
                 // r = computeObjectiveGradient(point)
                 req = REQ_G;
-#pragma unroll
-                for (int i = 0; i < K; ++i) xg[i] = point[i];
                 pc = PC_G0;
                 return;
             case PC_G0: {
@@ -706,11 +714,11 @@ struct CGLane {
                 double dl = 0.0;
 #pragma unroll
                 for (int i = 0; i < K; ++i) {
-                    dir[i] = xg[i];                       // steepestDescent = precondition(r) = r.clone()
-                    dl = dl + xg[i] * dir[i];
+                    dir[i] = grad[i];                     // steepestDescent = precondition(r) = r.clone()
+                    dl = dl + grad[i] * dir[i];
                 }
                 delta = dl;
-                memo_obj = f;                             // F(point) fused into the gradient pass
+                memo_obj = ev_val;                        // F(point) fused into the gradient pass
                 pc = PC_TOP;
                 break;
             }
@@ -805,14 +813,15 @@ struct CGLane {
                 pc = PC_BR_LOOP;
                 break;
             case PC_BR_END: {
+                // bracket -> Brent (shared storage: read everything needed before writing)
                 double lo = xA, hi = xC;
-                const double mid = xB;
+                const double mid = xB, fmid = fB;
                 if (lo > hi) { double t = lo; lo = hi; hi = t; }
                 if (lo >= hi || mid < lo || mid > hi) { fail(ARIMA_ST_BAD_INTERVAL); return; }  // SearchInterval
                 if (lo < hi) { a = lo; b = hi; } else { a = hi; b = lo; }
                 bx = bv = bw = mid;
                 bd = be = 0.0;
-                eval(mid, 0, 1, fB, PC_BRENT_FX);                        // fx = f(mid) (memo: bracket fMid)
+                eval(mid, 0, 1, fmid, PC_BRENT_FX);                      // fx = f(mid) (memo: bracket fMid)
                 break;
             }
             case PC_BRENT_FX:
@@ -892,14 +901,12 @@ struct CGLane {
                     point[i] = point[i] + step * dir[i];
                     pfin = pfin && finite(point[i]);
                 }
-                if (!pfin) {
+                if (!pfin) {                          // the gradient at a non-finite point is NaN: no pass
 #pragma unroll
-                    for (int i = 0; i < K; ++i) xg[i] = __builtin_nan("");
+                    for (int i = 0; i < K; ++i) grad[i] = __builtin_nan("");
                     pc = PC_G;
                     break;
                 }
-#pragma unroll
-                for (int i = 0; i < K; ++i) xg[i] = point[i];
                 req = REQ_G;
                 pc = PC_G;
                 return;
@@ -909,15 +916,15 @@ struct CGLane {
                 const double deltaOld = delta;
                 double dl = 0.0;
 #pragma unroll
-                for (int i = 0; i < K; ++i) dl = dl + xg[i] * xg[i];
+                for (int i = 0; i < K; ++i) dl = dl + grad[i] * grad[i];
                 delta = dl;
                 const double beta = delta / deltaOld;       // FLETCHER_REEVES
                 if (iter % K == 0 || beta < 0) {
 #pragma unroll
-                    for (int i = 0; i < K; ++i) dir[i] = xg[i];
+                    for (int i = 0; i < K; ++i) dir[i] = grad[i];
                 } else {
 #pragma unroll
-                    for (int i = 0; i < K; ++i) dir[i] = xg[i] + beta * dir[i];
+                    for (int i = 0; i < K; ++i) dir[i] = grad[i] + beta * dir[i];
                 }
                 pc = PC_TOP;
                 break;
@@ -932,54 +939,61 @@ struct CGLane {
                 if (ev_memo_ok) { ev_val = ev_memo; pc = ev_ret; break; }
                 bool fin = true;
 #pragma unroll
-                for (int i = 0; i < K; ++i) {
-                    xg[i] = point[i] + ev_alpha * dir[i];
-                    fin = fin && finite(xg[i]);
-                }
+                for (int i = 0; i < K; ++i) fin = fin && finite(point[i] + ev_alpha * dir[i]);
                 if (!fin) { ev_val = __builtin_nan(""); pc = ev_ret; break; }
                 rq_nspec = 0;
                 if constexpr (NS > 0) {
+                    // (static indexing only: the state never needs scratch)
                     const long long ab = __double_as_longlong(ev_alpha);
                     bool hit = false;
-                    for (int s = 0; s < sp_n; ++s)
-                        if (__double_as_longlong(sp_alpha[s]) == ab) { ev_val = sp_f[s]; hit = true; }
+#pragma unroll
+                    for (int s = 0; s < NS; ++s)
+                        if (s < sp_n && __double_as_longlong(sp_alpha[s]) == ab) { ev_val = sp_f[s]; hit = true; }
                     if (hit) { spec_hits++; pc = ev_ret; break; }
-                    // predict the bracket's next value-independent points (same expressions as below)
-                    double bb = 0.0, cc = 0.0;
-                    bool chain = true;
+                    // predict the bracket's next value-independent points (same expressions as above)
+                    double bb = 0.0, cc = 0.0, first = 0.0;
+                    bool chain = true, has_first = false;
                     switch (ev_ret) {
                     case PC_BR_FB:                                      // xC if fA <= fB, then the wLim chain
                         cc = xB + GOLD * (xB - xA);
-                        rq_spec[rq_nspec++] = cc;
+                        first = cc;
+                        has_first = true;
                         bb = xB;
                         break;
                     case PC_BR_FC: bb = xB; cc = xC; break;            // wLim chain from (xB, xC)
                     case PC_BR_SHIFT_EV: bb = xC; cc = w; break;       // the shift makes (xB, xC) = (xC, w)
                     case PC_BR_A1:                                      // no break: golden extension
-                        rq_spec[rq_nspec++] = xC + GOLD * (xC - xB);
+                        first = xC + GOLD * (xC - xB);
+                        has_first = true;
                         chain = false;
                         break;
                     case PC_BR_C1:                                      // fW > fC: golden extension from w
-                        rq_spec[rq_nspec++] = w + GOLD * (w - xC);
+                        first = w + GOLD * (w - xC);
+                        has_first = true;
                         chain = false;
                         break;
                     default: chain = false; break;
                     }
-                    while (chain && rq_nspec < NS) {
-                        const double nx = bb + GROW * (cc - bb);
-                        rq_spec[rq_nspec++] = nx;
-                        bb = cc;
-                        cc = nx;
+                    int cnt = 0;
+#pragma unroll
+                    for (int h = 0; h < NS; ++h) {
+                        if (h == 0 && has_first) {
+                            rq_spec[h] = first;
+                            cnt++;
+                        } else if (chain) {
+                            const double nx = bb + GROW * (cc - bb);
+                            rq_spec[h] = nx;
+                            bb = cc;
+                            cc = nx;
+                            cnt++;
+                        }
                     }
+                    rq_nspec = (uint8_t)cnt;
                 }
                 req = REQ_F;
-                pc = PC_EVAL_RESP;
+                pc = (uint8_t)ev_ret;                  // resume point once the response arrives
                 return;
             }
-            case PC_EVAL_RESP:
-                ev_val = f;
-                pc = ev_ret;
-                break;
             case PC_DONE:
             default:
                 return;
@@ -990,13 +1004,26 @@ struct CGLane {
 
 // LDS slot of one lane's optimizer state: padded to an odd number of 8-byte words so that 64 lanes reading the
 // same field with ds_read_b64 hit distinct bank pairs (stride = 8 * odd bytes; MI355X_MICROARCH.md LDS table).
-template <int K>
+template <int K, int NS>
 struct alignas(8) LaneSlot {
-    static constexpr int kWords = (int)((sizeof(CGLane<K>) + 7) / 8);
+    static constexpr int kWords = (int)((sizeof(CGLane<K, NS>) + 7) / 8);
     static constexpr int kPadWords = (kWords % 2 == 0) ? 1 : 2;   // total word count odd
-    CGLane<K> s;
+    CGLane<K, NS> s;
     double pad[kPadWords];
 };
+
+// Waves per workgroup of the fit kernel (one workgroup per CU, 64 lanes per wave): as many as the LDS slots of
+// 64 lanes fit in 160 KiB, at most STS_CG_MAX_WAVES (4 = one per SIMD: measured faster than two per SIMD,
+// which halves the pass's register budget and doubles the in-flight streams per CU).
+#ifndef STS_CG_MAX_WAVES
+#define STS_CG_MAX_WAVES 4
+#endif
+template <int K, int NS>
+constexpr int cg_waves() {
+    constexpr int per_wave = 64 * (int)sizeof(LaneSlot<K, NS>);
+    constexpr int w = 163840 / per_wave;
+    return w > STS_CG_MAX_WAVES ? STS_CG_MAX_WAVES : (w < 1 ? 1 : w);
+}
 
 // ------------------------------------------------------------------------------------------------------
 // Philox4x32-10 (counter-based) + Box-Muller for the synthetic generator

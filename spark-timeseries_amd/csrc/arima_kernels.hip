@@ -192,6 +192,12 @@ int launch_sample(double *out, int64_t ld, int64_t N, int T, int p, int d, int q
     return ARIMA_OK;
 }
 
+#ifdef STS_DEV
+STS_DECLARE_P(STS_DEV_P, extern)
+#define STS_P_SWITCH(CALL)                                                                                 \
+    if (p == STS_DEV_P) return CALL(STS_DEV_P);                                                            \
+    return ARIMA_E_UNSUPPORTED;
+#else
 STS_DECLARE_P(0, extern)
 STS_DECLARE_P(1, extern)
 STS_DECLARE_P(2, extern)
@@ -209,6 +215,7 @@ STS_DECLARE_P(5, extern)
     case 5: return CALL(5);                                                                                \
     default: return ARIMA_E_UNSUPPORTED;                                                                   \
     }
+#endif
 
 int launch_hr_init(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, double *init_out,
                    int32_t *status_out, hipStream_t s) {

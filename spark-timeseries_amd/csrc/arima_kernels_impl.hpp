@@ -151,38 +151,69 @@ __device__ __forceinline__ void write_fit(int64_t sid, int status, const double 
     if (flags_out) flags_out[sid] = ok ? flags : 0;
 }
 
-// One workgroup of 256 lanes per CU (1 wave per SIMD): every lane's optimizer state lives in LDS
-// (LaneSlot<K>, ~90-150 KB per workgroup), so the registers are free for the pass: its working set plus a
-// kPrefetchF-deep ring of 128-B chunks per lane, which is what keeps HBM busy at this occupancy.
-template <int P, int Q, int I, bool SMEAR>
-__global__ __launch_bounds__(256, 1) void k_cg_fit(const double *__restrict__ y, int64_t ld, int n, int64_t N,
-                                                   const double *__restrict__ init,
-                                                   const int32_t *__restrict__ init_status,
-                                                   double *__restrict__ coef_out, double *__restrict__ ll_out,
-                                                   int32_t *__restrict__ status_out,
-                                                   int32_t *__restrict__ n_eval_out,
-                                                   int32_t *__restrict__ n_grad_out, uint8_t *__restrict__ flags_out,
-                                                   unsigned long long *__restrict__ ctl, int g_permille) {
+// Persistent fit kernel: one workgroup of 64 * WAVES lanes per CU (WAVES = cg_waves<K, NS>(), up to two waves
+// per SIMD). Every lane's optimizer state lives in LDS (LaneSlot), so the registers are free for the pass.
+// Per wave iteration: (1) every lane with a response advances its state machine to its next request (finished
+// lanes write their result and start the next series, whose id and initial point were fetched one series
+// ahead); (2) the wave runs one pass over every served lane's own series. A gradient pass costs several
+// objective passes, so lanes that want G sit out objective-only passes until at least g_permille/1000 of the
+// active lanes want G (or nobody wants F); a G pass also yields the objective, so F lanes are served by it too.
+template <int P, int Q, int I, bool SMEAR, int WAVES>
+__global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void k_cg_fit(
+    const double *__restrict__ y, int64_t ld, int n, int64_t N, const double *__restrict__ init,
+    const int32_t *__restrict__ init_status, double *__restrict__ coef_out, double *__restrict__ ll_out,
+    int32_t *__restrict__ status_out, int32_t *__restrict__ n_eval_out, int32_t *__restrict__ n_grad_out,
+    uint8_t *__restrict__ flags_out, unsigned long long *__restrict__ ctl, int g_permille) {
     // ctl[0] = work counter, ctl[1] = lane F passes, ctl[2] = lane G passes, ctl[3] = wave F-only passes,
-    // ctl[4] = wave G passes, ctl[5] = objective evaluations, ctl[6] = gradient evaluations
+    // ctl[4] = wave G passes, ctl[5] = objective evaluations, ctl[6] = gradient evaluations, ctl[7] = spec
+    // hits, ctl[8] = wave multi-point passes, ctl[10..14] = STS_TIMING diagnostics
     constexpr int K = I + P + Q;
-    __shared__ LaneSlot<K> slots[256];
-    CGLane<K> &L = slots[threadIdx.x].s;
+    constexpr int NS = spec_slots<K>();
+    __shared__ LaneSlot<K, NS> slots[64 * WAVES];
+    CGLane<K, NS> &L = slots[threadIdx.x].s;
     int64_t sid = -1;
     bool idle = false, need_new = true;
     const double *row = y;
     unsigned long long lane_f = 0, lane_g = 0, wave_f = 0, wave_g = 0, wave_m = 0, evals = 0, grads = 0, hits = 0;
     const bool lane0 = (threadIdx.x & 63) == 0;
+    // response of the last served request (registers)
+    double resp_f = 0.0, resp_g[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) resp_g[j] = 0.0;
+    // next series of this lane, fetched one series ahead (id, then its status and initial point)
+    int64_t nxt = (int64_t)atomicAdd(&ctl[0], 1ull);
+    bool nxt_loaded = false;
+    int nxt_st = ARIMA_ST_OK;
+    double nxt_x0[K];
     L.req = REQ_NONE;
+#ifdef STS_TIMING
+    unsigned long long t_adv = 0, t_pass = 0, t_g = 0, t_m = 0;
+    int kind = 0;
+    const unsigned long long t_birth = __builtin_amdgcn_s_memtime();
+#endif
     for (;;) {
+#ifdef STS_TIMING
+        const unsigned long long t_a0 = __builtin_amdgcn_s_memtime();
+#endif
+        if (!nxt_loaded && nxt < N) {                 // prefetch the next series' initial point
+            nxt_st = init_status ? init_status[nxt] : ARIMA_ST_OK;
+#pragma unroll
+            for (int j = 0; j < K; ++j) nxt_x0[j] = init[nxt * K + j];
+            nxt_loaded = true;
+        }
         // ---- per lane: advance the state machine to its next request (refilling finished lanes) ----
         while (!idle) {
             if (need_new) {
-                sid = (int64_t)atomicAdd(&ctl[0], 1ull);
-                if (sid >= N) { idle = true; break; }
+                if (nxt >= N) { idle = true; break; }
+                sid = nxt;
+                const int st0 = nxt_st;
+                double x0[K];
+#pragma unroll
+                for (int j = 0; j < K; ++j) x0[j] = nxt_x0[j];
+                nxt = (int64_t)atomicAdd(&ctl[0], 1ull);
+                nxt_loaded = false;
                 need_new = false;
                 row = y + sid * ld;
-                const int st0 = init_status ? init_status[sid] : ARIMA_ST_OK;
                 if (st0 != ARIMA_ST_OK) {
                     double nanc[K];
 #pragma unroll
@@ -190,15 +221,18 @@ __global__ __launch_bounds__(256, 1) void k_cg_fit(const double *__restrict__ y,
                     write_fit<K>(sid, st0, nanc, 0.0, 0, 0, 0, coef_out, ll_out, status_out, n_eval_out,
                                  n_grad_out, flags_out);
                     need_new = true;
+                    if (nxt < N) {                    // (rare) the next one is needed right away
+                        nxt_st = init_status ? init_status[nxt] : ARIMA_ST_OK;
+#pragma unroll
+                        for (int j = 0; j < K; ++j) nxt_x0[j] = init[nxt * K + j];
+                        nxt_loaded = true;
+                    }
                     continue;
                 }
-                double x0[K];
-#pragma unroll
-                for (int j = 0; j < K; ++j) x0[j] = init[sid * K + j];
                 L.start(x0);
             }
             if (L.req != REQ_NONE) break;        // request still pending (deferred G): nothing to advance
-            L.advance();
+            L.advance(resp_f, resp_g);
             if (L.done()) {
                 double pt[K];
 #pragma unroll
@@ -210,15 +244,23 @@ __global__ __launch_bounds__(256, 1) void k_cg_fit(const double *__restrict__ y,
                 grads += L.n_grad;
                 hits += L.spec_hits;
                 need_new = true;
+                if (!nxt_loaded && nxt < N) {
+                    nxt_st = init_status ? init_status[nxt] : ARIMA_ST_OK;
+#pragma unroll
+                    for (int j = 0; j < K; ++j) nxt_x0[j] = init[nxt * K + j];
+                    nxt_loaded = true;
+                }
                 continue;
             }
             break;
         }
         // ---- per wave: one pass serving the posted requests ----
         const unsigned long long act = __ballot(!idle);
+#ifdef STS_TIMING
+        const unsigned long long t_p0 = __builtin_amdgcn_s_memtime();
+        t_adv += t_p0 - t_a0;
+#endif
         if (act == 0ull) break;
-        // G-pass policy: a gradient pass costs several objective passes; lanes waiting for G sit out F-only
-        // passes until at least g_permille/1000 of the active lanes want G (or nobody wants F).
         const int req = idle ? REQ_NONE : L.req;
         const unsigned long long wantG = __ballot(req == REQ_G);
         const int nG = __popcll(wantG), nA = __popcll(act);
@@ -227,14 +269,20 @@ __global__ __launch_bounds__(256, 1) void k_cg_fit(const double *__restrict__ y,
         const bool served = !idle && (anyG || req == REQ_F);
         const double *prow = served ? row : y;
         double c[K], css, g[K];
+        if (served) {
+            L.request_point(c);
+        } else {
 #pragma unroll
-        for (int j = 0; j < K; ++j) c[j] = served ? L.xg[j] : 0.0;
-        constexpr int NS = CGLane<K>::NS;
+            for (int j = 0; j < K; ++j) c[j] = 0.0;
+        }
         const int nspec = (served && req == REQ_F) ? L.rq_nspec : 0;
         const bool anySpec = NS > 0 && !anyG && __ballot(nspec > 0) != 0ull;
         if (anyG) {
             css_pass<P, Q, I, true, SMEAR>(prow, n, c, css, g);
             wave_g += lane0;
+#ifdef STS_TIMING
+            kind = 1;
+#endif
         } else if constexpr (NS > 0) {
             if (anySpec) {
                 // primary point + the lane's speculative points (lanes with fewer repeat the primary)
@@ -250,12 +298,18 @@ __global__ __launch_bounds__(256, 1) void k_cg_fit(const double *__restrict__ y,
                 }
                 css_pass_multi<P, Q, I, NS + 1>(prow, n, cm, cssm);
                 css = cssm[0];
-                for (int h = 0; h < nspec; ++h) {
-                    L.sp_alpha[h] = L.rq_spec[h];
-                    L.sp_f[h] = css_to_loglik(cssm[h + 1], n);
+#pragma unroll
+                for (int h = 0; h < NS; ++h) {
+                    if (h < nspec) {
+                        L.sp_alpha[h] = L.rq_spec[h];
+                        L.sp_f[h] = css_to_loglik(cssm[h + 1], n);
+                    }
                 }
-                if (nspec > 0) L.sp_n = nspec;
+                if (nspec > 0) L.sp_n = (uint8_t)nspec;
                 wave_m += lane0;
+#ifdef STS_TIMING
+                kind = 2;
+#endif
             } else {
                 css_pass<P, Q, I, false, SMEAR>(prow, n, c, css, g);
                 wave_f += lane0;
@@ -265,17 +319,35 @@ __global__ __launch_bounds__(256, 1) void k_cg_fit(const double *__restrict__ y,
             wave_f += lane0;
         }
         if (served) {
-            L.f = css_to_loglik(css, n);
+            resp_f = css_to_loglik(css, n);
             if (req == REQ_G) {
 #pragma unroll
-                for (int j = 0; j < K; ++j) L.xg[j] = g[j];
+                for (int j = 0; j < K; ++j) resp_g[j] = g[j];
                 lane_g++;
             } else {
                 lane_f++;
             }
             L.req = REQ_NONE;
         }
+#ifdef STS_TIMING
+        {
+            const unsigned long long dt = __builtin_amdgcn_s_memtime() - t_p0;
+            t_pass += dt;
+            if (kind == 1) t_g += dt;
+            if (kind == 2) t_m += dt;
+            kind = 0;
+        }
+#endif
     }
+#ifdef STS_TIMING
+    if (lane0) {
+        atomicAdd(&ctl[10], t_adv);
+        atomicAdd(&ctl[11], t_pass);
+        atomicAdd(&ctl[12], __builtin_amdgcn_s_memtime() - t_birth);
+        atomicAdd(&ctl[13], t_g);
+        atomicAdd(&ctl[14], t_m);
+    }
+#endif
     atomicAdd(&ctl[1], lane_f);
     atomicAdd(&ctl[2], lane_g);
     if (lane0) {
@@ -340,6 +412,17 @@ __global__ __launch_bounds__(256) void k_model_flags(const double *__restrict__ 
 template <int V>
 using IC = std::integral_constant<int, V>;
 
+#ifdef STS_DEV
+// dev build (make dev): only q = STS_DEV_Q, smear off -- fast compiles for kernel experiments
+template <class Fn>
+int with_order(int v, Fn &&fn) {
+    return v == STS_DEV_Q ? fn(IC<STS_DEV_Q>{}) : ARIMA_E_UNSUPPORTED;
+}
+template <class Fn>
+int with_smear(int v, Fn &&fn) {
+    return v ? ARIMA_E_UNSUPPORTED : fn(IC<0>{});
+}
+#else
 template <class Fn>
 int with_order(int v, Fn &&fn) {
     switch (v) {
@@ -352,10 +435,17 @@ int with_order(int v, Fn &&fn) {
     default: return ARIMA_E_UNSUPPORTED;
     }
 }
+#endif
 template <class Fn>
 int with_bool(int v, Fn &&fn) {
     return v ? fn(IC<1>{}) : fn(IC<0>{});
 }
+#ifndef STS_DEV
+template <class Fn>
+int with_smear(int v, Fn &&fn) {
+    return with_bool(v, fn);
+}
+#endif
 
 inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
 
@@ -403,15 +493,16 @@ int launch_cg_fit_P(const double *y, int64_t ld, int n, int64_t N, int q, int I,
                     int grid_blocks, int g_permille, hipStream_t s) {
     return with_order(q, [&](auto Qc) {
         return with_bool(I, [&](auto Ic) {
-            return with_bool(smear, [&](auto Sc) {
+            return with_smear(smear, [&](auto Sc) {
                 constexpr int Q = decltype(Qc)::value, II = decltype(Ic)::value;
                 constexpr bool S = decltype(Sc)::value != 0;
                 if constexpr (P + Q + II == 0) {
                     return ARIMA_E_INVALID_ARG;
                 } else {
-                    hipLaunchKernelGGL((k_cg_fit<P, Q, II, S>), dim3(grid_blocks), dim3(256), 0, s, y, ld, n, N, init,
-                                       init_status, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out,
-                                       ctl, g_permille);
+                    constexpr int W = cg_waves<P + Q + II, spec_slots<P + Q + II>()>();
+                    hipLaunchKernelGGL((k_cg_fit<P, Q, II, S, W>), dim3(grid_blocks), dim3(64 * W), 0, s, y, ld, n, N,
+                                       init, init_status, coef_out, ll_out, status_out, n_eval_out, n_grad_out,
+                                       flags_out, ctl, g_permille);
                     STS_CHECK_LAUNCH();
                     return ARIMA_OK;
                 }
@@ -425,11 +516,12 @@ int cg_fit_occupancy_blocks_P(int q, int I, int smear) {
     int blocks = 0;
     with_order(q, [&](auto Qc) {
         return with_bool(I, [&](auto Ic) {
-            return with_bool(smear, [&](auto Sc) {
+            return with_smear(smear, [&](auto Sc) {
                 constexpr int Q = decltype(Qc)::value, II = decltype(Ic)::value;
                 constexpr bool S = decltype(Sc)::value != 0;
                 if constexpr (P + Q + II > 0) {
-                    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_cg_fit<P, Q, II, S>, 256, 0);
+                    constexpr int W = cg_waves<P + Q + II, spec_slots<P + Q + II>()>();
+                    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_cg_fit<P, Q, II, S, W>, 64 * W, 0);
                 }
                 return 0;
             });
@@ -457,7 +549,7 @@ int launch_css_grad_P(const double *y, int64_t ld, int n, int64_t N, int q, int 
                       double *g_out, hipStream_t s) {
     return with_order(q, [&](auto Qc) {
         return with_bool(I, [&](auto Ic) {
-            return with_bool(smear, [&](auto Sc) {
+            return with_smear(smear, [&](auto Sc) {
                 constexpr int Q = decltype(Qc)::value, II = decltype(Ic)::value;
                 constexpr bool S = decltype(Sc)::value != 0;
                 hipLaunchKernelGGL((k_css_grad<P, Q, II, S>), dim3(grid_for(N, 256)), dim3(256), 0, s, y, ld, n, N,

@@ -272,6 +272,7 @@ static int fit_device_locked(arima_handle *h, const double *d_series, int64_t N,
     st.spec_hits = (int64_t)c[7];
     st.wave_multi_passes = (int64_t)c[8];
     st.grid_blocks = h->last_grid;
+    for (int i = 0; i < 6; ++i) st.diag[i] = (int64_t)c[10 + i];
     // HR passes: 2 per column of each of the two least squares (+1 re-transform sweep over C rows)
     const int M = std::max(p, q), m = M + 1;
     if (p > 0 && q == 0) st.hr_passes = N * (int64_t)(2 * (I + p));

@@ -53,10 +53,12 @@ class FitStats(ctypes.Structure):
                 ("flops", ctypes.c_double), ("ms_difference", ctypes.c_double), ("ms_hr_init", ctypes.c_double),
                 ("ms_cg_fit", ctypes.c_double), ("ms_total", ctypes.c_double),
                 ("wave_f_passes", ctypes.c_int64), ("wave_g_passes", ctypes.c_int64), ("grid_blocks", ctypes.c_int64),
-                ("spec_hits", ctypes.c_int64), ("wave_multi_passes", ctypes.c_int64)]
+                ("spec_hits", ctypes.c_int64), ("wave_multi_passes", ctypes.c_int64), ("diag", ctypes.c_int64 * 6)]
 
     def as_dict(self):
-        return {name: getattr(self, name) for name, _ in self._fields_}
+        d = {name: getattr(self, name) for name, _ in self._fields_}
+        d["diag"] = list(self.diag)
+        return d
 
 
 class EngineError(RuntimeError):
