@@ -78,6 +78,160 @@ __global__ __launch_bounds__(256) void k_inverse_difference(const double *__rest
 }
 
 // =======================================================================================================
+// ARIMAModel.forecast (ARIMA.scala:696-764), one lane per series, one streaming pass over the row.
+// Every quantity the reference materialises as an array is carried in registers instead:
+//   Dc[r]  = D(r, t), the ping-pong differencing column (differencesOfOrderD, :700)
+//   Mc[r]  = diffMatrix(r, t) (:731-743): like D except diffMatrix(r, r) copies diffMatrix(r-1, r)
+//   xr[j]  = ext(cur-1-j)  (ext = [c]*M ++ diffed, :703-707), hr[j] = hist(cur-1-j) (iterateARMA result :708)
+//   sr[j]  = column sums of diffMatrix(0 until d, t-j) (:745-751), delayed d+1 steps to meet hist(M+idx)
+// Same operations in the same order as the oracle's restatement (oracle/arima_oracle.c orc_forecast), so the
+// result is bit-identical. The final inverseDifferencesOfOrderD over [T-d, T+nFuture) runs in place on the
+// lane's own output row.
+// =======================================================================================================
+constexpr int kFcMaxOrder = 5;   // p, q <= 5 (check_orders)
+constexpr int kFcMaxD = 8;
+
+__global__ __launch_bounds__(256) void k_forecast(const double *__restrict__ ts_all, int64_t ld_in,
+                                                  const double *__restrict__ coef_all, int k,
+                                                  double *__restrict__ out_all, int64_t ld_out, int64_t N, int T,
+                                                  int p, int d, int q, int I, int nF) {
+    const int64_t sid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (sid >= N) return;
+    const double *ts = ts_all + sid * ld_in;
+    double *out = out_all + sid * ld_out;
+    const int M = p > q ? p : q;
+    // coefficients [c?, phi_1..phi_p, theta_1..theta_q] (ARIMA.scala:74-77); k == 0 reads nothing
+    const double *cf = coef_all + sid * k;
+    const double c0 = k > 0 ? cf[0] : 0.0;
+    double phi[kFcMaxOrder], th[kFcMaxOrder];
+#pragma unroll
+    for (int j = 0; j < kFcMaxOrder; ++j) {
+        phi[j] = j < p ? cf[I + j] : 0.0;
+        th[j] = j < q ? cf[I + p + j] : 0.0;
+    }
+    const double ia = I ? c0 : 0.0;
+    double xr[kFcMaxOrder], hr[kFcMaxOrder], ma[kFcMaxOrder];
+#pragma unroll
+    for (int j = 0; j < kFcMaxOrder; ++j) { xr[j] = ia; hr[j] = 0.0; ma[j] = 0.0; }
+    double Dc[kFcMaxD + 1], Dp[kFcMaxD + 1], Mc[kFcMaxD], Mp[kFcMaxD], sr[kFcMaxD + 2];
+#pragma unroll
+    for (int r = 0; r <= kFcMaxD; ++r) { Dc[r] = 0.0; Dp[r] = 0.0; }
+#pragma unroll
+    for (int r = 0; r < kFcMaxD; ++r) { Mc[r] = 0.0; Mp[r] = 0.0; }
+#pragma unroll
+    for (int j = 0; j < kFcMaxD + 2; ++j) sr[j] = 0.0;
+
+    for (int t = 0; t < T; ++t) {
+        const double v = ts[t];
+        // differencing column t (UnivariateTimeSeries.scala:384-405 pass r: out(t) = in(t) - in(t-1) for t >= r)
+        Dc[0] = v;
+#pragma unroll
+        for (int r = 1; r <= kFcMaxD; ++r)
+            if (r <= d) Dc[r] = t < r ? Dc[r - 1] : Dc[r - 1] - Dp[r - 1];
+        // diffMatrix column t and its column sum (d > 0 only)
+        double s = 0.0;
+        if (d > 0) {
+            Mc[0] = v;
+#pragma unroll
+            for (int r = 1; r < kFcMaxD; ++r)
+                if (r < d) Mc[r] = t < r ? 0.0 : (t == r ? Mc[r - 1] : Mc[r - 1] - Mp[r - 1]);
+#pragma unroll
+            for (int r = 0; r < kFcMaxD; ++r)
+                if (r < d) s = s + Mc[r];
+#pragma unroll
+            for (int j = kFcMaxD + 1; j >= 1; --j) sr[j] = sr[j - 1];
+            sr[0] = s;
+#pragma unroll
+            for (int r = 0; r < kFcMaxD; ++r) Mp[r] = Mc[r];
+        }
+#pragma unroll
+        for (int r = 0; r <= kFcMaxD; ++r) Dp[r] = Dc[r];
+        if (t < d) out[t] = v;                                       // :724
+        if (t >= d) {
+            // iterateARMA(ext, hist, +, goldStandard = ext) step at ext index M + i, i = t - d (:708, :581-618)
+            const int i = t - d;
+            const double y = Dc[d];
+            double f = 0.0;
+            f = f + (double)I * c0;
+#pragma unroll
+            for (int j = 0; j < kFcMaxOrder; ++j)
+                if (j < p) f = f + xr[j] * phi[j];
+#pragma unroll
+            for (int j = 0; j < kFcMaxOrder; ++j)
+                if (j < q) f = f + ma[j] * th[j];
+            const double err = y - f;
+#pragma unroll
+            for (int j = kFcMaxOrder - 1; j >= 1; --j)                 // updateMAErrors (:544-554): smear
+                if (j < q) ma[j] = ma[0];
+            if (q > 0) ma[0] = err;
+#pragma unroll
+            for (int j = kFcMaxOrder - 1; j >= 1; --j) { xr[j] = xr[j - 1]; hr[j] = hr[j - 1]; }
+            xr[0] = y;
+            hr[0] = f;
+            if (d == 0) {
+                out[i] = f;                                            // :726
+            } else if (i >= d && i < T - d) {
+                double sd = 0.0;                                       // column sum at i - 1 = t - d - 1
+#pragma unroll
+                for (int j = 0; j < kFcMaxD + 2; ++j)
+                    if (j == d + 1) sd = sr[j];
+                out[i] = sd + f;                                       // :745-751
+            }
+        }
+        if (d > 0 && t >= T - d) {                                     // diag(diffMatrix(0 until d, -d to -1))
+            const int r = t - (T - d);
+            double dg = 0.0;
+#pragma unroll
+            for (int j = 0; j < kFcMaxD; ++j)
+                if (j == r) dg = Mc[j];
+            out[t] = dg;
+        }
+    }
+    // forward = hist(-M..) ++ zeros(nFuture); iterateARMA(forward, forward, +, gold = forward, maTerms) (:711-720)
+    double fr[kFcMaxOrder], mt[kFcMaxOrder];
+#pragma unroll
+    for (int j = 0; j < kFcMaxOrder; ++j) {
+        fr[j] = hr[j];                                                 // fwd(i-1-j)
+        mt[j] = 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < kFcMaxOrder; ++j)                              // maTerms(j) = ext(L-M+j) - hist(L-M+j)
+        if (j < M) {
+            double xv = 0.0, hv = 0.0;
+#pragma unroll
+            for (int jj = 0; jj < kFcMaxOrder; ++jj)
+                if (jj == M - 1 - j) { xv = xr[jj]; hv = hr[jj]; }
+            mt[j] = xv - hv;
+        }
+    double *fo = out + T;
+    for (int i = 0; i < nF; ++i) {
+        double f = 0.0;
+        f = f + (double)I * c0;
+#pragma unroll
+        for (int j = 0; j < kFcMaxOrder; ++j)
+            if (j < p) f = f + fr[j] * phi[j];
+#pragma unroll
+        for (int j = 0; j < kFcMaxOrder; ++j)
+            if (j < q) f = f + mt[j] * th[j];
+        const double err = f - f;
+#pragma unroll
+        for (int j = kFcMaxOrder - 1; j >= 1; --j)                     // updateMAErrors over maTerms' length M
+            if (j < M) mt[j] = mt[0];
+        if (M > 0) mt[0] = err;
+#pragma unroll
+        for (int j = kFcMaxOrder - 1; j >= 1; --j) fr[j] = fr[j - 1];
+        fr[0] = f;
+        fo[i] = f;                                                     // :728
+    }
+    if (d > 0) {                                                       // inverseDifferencesOfOrderD (:756-761)
+        double *w = out + (T - d);
+        const int L = d + nF;
+        for (int lvl = d; lvl >= 1; --lvl)
+            for (int j = lvl; j < L; ++j) w[j] = w[j] + w[j - 1];
+    }
+}
+
+// =======================================================================================================
 // Synthetic generator: ARIMAModel.sample (ARIMA.scala:655-678) with per-series jittered coefficients
 // =======================================================================================================
 constexpr int kSampleMaxOrder = 8;
@@ -178,6 +332,17 @@ int launch_inverse_difference(const double *in, int64_t ld_in, double *out, int6
     if (N == 0) return ARIMA_OK;
     hipLaunchKernelGGL(k_inverse_difference, dim3(grid_for(N, 256)), dim3(256), 0, s, in, ld_in, out, ld_out, N,
                        T, d);
+    STS_CHECK_LAUNCH();
+    return ARIMA_OK;
+}
+
+int launch_forecast(const double *ts, int64_t ld_in, const double *coef, int k, double *out, int64_t ld_out,
+                    int64_t N, int T, int p, int d, int q, int I, int n_future, hipStream_t s) {
+    if (N == 0) return ARIMA_OK;
+    if (p > kFcMaxOrder || q > kFcMaxOrder || d > kFcMaxD) return ARIMA_E_UNSUPPORTED;
+    if (T < d || n_future < 0 || k != I + p + q || ld_out < (int64_t)T + n_future) return ARIMA_E_INVALID_ARG;
+    hipLaunchKernelGGL(k_forecast, dim3(grid_for(N, 256)), dim3(256), 0, s, ts, ld_in, coef, k, out, ld_out, N, T,
+                       p, d, q, I, n_future);
     STS_CHECK_LAUNCH();
     return ARIMA_OK;
 }

@@ -8,6 +8,8 @@ namespace sts {
 
 int launch_difference(const double *in, int64_t ld_in, double *out, int64_t ld_out, int64_t N, int T, int d,
                       int drop, hipStream_t s);
+int launch_forecast(const double *ts, int64_t ld_in, const double *coef, int k, double *out, int64_t ld_out,
+                    int64_t N, int T, int p, int d, int q, int I, int n_future, hipStream_t s);
 int launch_inverse_difference(const double *in, int64_t ld_in, double *out, int64_t ld_out, int64_t N, int T,
                               int d, hipStream_t s);
 int launch_hr_init(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, double *init_out,

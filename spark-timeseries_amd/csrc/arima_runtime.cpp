@@ -480,11 +480,28 @@ int arima_model_flags_batch(arima_handle *h, const double *coef, int64_t N, int3
     return ARIMA_OK;
 }
 
-int arima_forecast_batch(arima_handle *h, const double *series, int64_t n_series, int32_t T, int32_t p, int32_t d,
-                         int32_t q, int32_t include_intercept, const double *coef, int32_t n_future, double *out) {
-    (void)series; (void)n_series; (void)T; (void)p; (void)d; (void)q; (void)include_intercept; (void)coef;
-    (void)n_future; (void)out;
-    return set_err(h, ARIMA_E_UNSUPPORTED, "forecast: not built yet");
+int arima_forecast_batch(arima_handle *h, const double *series, int64_t N, int32_t T, int32_t p, int32_t d,
+                         int32_t q, int32_t I, const double *coef, int32_t n_future, double *out) {
+    if (!h) return ARIMA_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    RCCHK(h, check_orders(h, p, d, q, I), "orders");
+    if (N < 0 || T < d || n_future < 0) return set_err(h, ARIMA_E_INVALID_ARG, "bad shape");
+    if (N == 0) return ARIMA_OK;
+    if (!series || !coef || !out) return set_err(h, ARIMA_E_INVALID_ARG, "null buffer");
+    HIPCHK(h, hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    const int k = I + p + q;
+    const int64_t L = (int64_t)T + n_future;
+    RCCHK(h, h->h_series.ensure((size_t)N * std::max(T, 1) * sizeof(double)), "staging");
+    RCCHK(h, h->h_coef.ensure((size_t)N * std::max(k, 1) * sizeof(double)), "staging");
+    RCCHK(h, h->h_aux.ensure((size_t)N * std::max<int64_t>(L, 1) * sizeof(double)), "staging");
+    if (T > 0) HIPCHK(h, hipMemcpyAsync(h->h_series.ptr, series, (size_t)N * T * sizeof(double), hipMemcpyHostToDevice, s));
+    if (k > 0) HIPCHK(h, hipMemcpyAsync(h->h_coef.ptr, coef, (size_t)N * k * sizeof(double), hipMemcpyHostToDevice, s));
+    RCCHK(h, sts::launch_forecast(h->h_series.as<double>(), T, h->h_coef.as<double>(), k, h->h_aux.as<double>(), L, N,
+                                  T, p, d, q, I, n_future, s), "forecast");
+    if (L > 0) HIPCHK(h, hipMemcpyAsync(out, h->h_aux.ptr, (size_t)N * L * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    return ARIMA_OK;
 }
 
 int arima_sample_batch_device(arima_handle *h, double *d_series, int64_t N, int32_t T, int64_t ld, int32_t p,

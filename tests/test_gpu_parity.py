@@ -197,3 +197,54 @@ def test_python_mirror_api(engine):
     out = list(fit_arima_partition(recs, 1, 0, 1))
     assert [k for k, _ in out] == ["a", "b", "c"]
     assert np.array_equal(out[0][1], arr["coef"][0]) and np.array_equal(out[2][1], arr["coef"][0])
+
+
+# ---- ARIMAModel.forecast (ARIMA.scala:696-764): bit-identical to the oracle on every order the build compiles ----
+FORECAST_CASES = [(0, 0, 0, 1), (1, 0, 1, 1), (2, 1, 2, 1), (2, 1, 2, 0), (1, 2, 0, 1), (0, 1, 3, 1), (3, 3, 1, 0),
+                  (5, 1, 5, 1), (4, 2, 2, 1), (0, 2, 0, 1), (1, 8, 1, 1)]
+
+
+@pytest.mark.parametrize("pdqi", FORECAST_CASES)
+@pytest.mark.parametrize("n_future", [0, 1, 17])
+def test_forecast_bit_exact(engine, pdqi, n_future):
+    p, d, q, I = pdqi
+    rng = np.random.default_rng(1000 + 97 * p + 13 * d + q + I + n_future)
+    N, T = 96, 211
+    s = rng.standard_normal((N, T)).cumsum(axis=1) * 3.0 + 5.0
+    coef = rng.uniform(-0.6, 0.6, (N, p + q + I))
+    out = engine.forecast(s, p, d, q, I, coef, n_future)
+    exp = np.stack([O.forecast(s[i], p, d, q, I, coef[i], n_future) for i in range(N)])
+    assert out.shape == (N, T + n_future)
+    assert _same(out, exp), (pdqi, n_future, np.nanmax(np.abs(out - exp)))
+
+
+@pytest.mark.parametrize("T", [2, 3, 4, 6])
+def test_forecast_short_series(engine, T):
+    # series barely longer than d and shorter than max(p, q): the prefix/diag regions overlap (C-9 edge cases)
+    rng = np.random.default_rng(T)
+    for p, d, q, I in [(2, 2, 3, 1), (5, 1, 5, 0), (1, 2, 1, 1)]:
+        if T < d:
+            continue
+        s = rng.standard_normal((8, T))
+        coef = rng.uniform(-0.5, 0.5, (8, p + q + I))
+        out = engine.forecast(s, p, d, q, I, coef, 5)
+        exp = np.stack([O.forecast(s[i], p, d, q, I, coef[i], 5) for i in range(8)])
+        assert _same(out, exp), (T, p, d, q, I)
+
+
+def test_forecast_of_fitted_model(engine):
+    # fit -> forecast on the C2 workload, and the ARIMA(0,0,0) mean KAT (ARIMASuite.scala:122-132) through the GPU
+    N, T = 512, 1024
+    s = _device_sample(engine, N, T, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 20261015).cpu().numpy()
+    res = engine.fit_batch(s, 2, 1, 2, True)
+    ok = res["status"] == 0
+    f = engine.forecast(s[ok], 2, 1, 2, True, res["coef"][ok], 30)
+    exp = np.stack([O.forecast(s[ok][i], 2, 1, 2, 1, res["coef"][ok][i], 30) for i in range(int(ok.sum()))])
+    assert np.all(np.abs(f - exp) <= 1e-6 * np.abs(exp))      # north_star: forecasts within 1e-6 relative
+    assert _same(f, exp)
+    from sparkts_amd.models import ARIMA
+    meta, arr = load_case("kat_ds1_101")
+    m = ARIMA.fit_model(0, 0, 0, arr["series"][0])
+    fc = m.forecast(arr["series"][0], 10)
+    mean = arr["series"][0].sum() / arr["series"][0].size
+    assert np.all(np.abs(np.ravel(fc)[-10:] - mean) < 1e-4)
