@@ -139,6 +139,21 @@ int arima_forecast_batch(arima_handle *h, const double *series, int64_t n_series
 int arima_model_flags_batch(arima_handle *h, const double *coef, int64_t n_series, int32_t p, int32_t q,
                             int32_t include_intercept, uint8_t *flags_out);
 
+/* ---- order search (BASELINE config C5; ARIMA.autoFit's selection rule, ARIMA.scala:280-375)
+ * Fits every (d, p, q, intercept) with d in [0,max_d], p in [0,max_p], q in [0,max_q] and intercept per
+ * intercept_mode (0: without, 1: with, 2: both), in that lexicographic order, and keeps per series the fit
+ * with the smallest approxAIC (ARIMA.scala:826-830) among those that returned normally and are stationary and
+ * invertible (the isStationary && isInvertible filter, ARIMA.scala:342); ties keep the first.
+ * order_out N x 4 = (p, d, q, intercept), -1s when no candidate qualified; coef_out N x 11 (zero-padded, NaN
+ * when none); aic_out N (+inf when none). Host buffers; the _device variant takes device pointers.          */
+int arima_order_search_batch(arima_handle *h, const double *series, int64_t n_series, int32_t T,
+                             int32_t max_p, int32_t max_d, int32_t max_q, int32_t intercept_mode, int32_t method,
+                             int32_t *order_out, double *coef_out, double *aic_out);
+int arima_order_search_batch_device(arima_handle *h, const double *d_series, int64_t n_series, int32_t T,
+                                    int64_t ld, int32_t max_p, int32_t max_d, int32_t max_q,
+                                    int32_t intercept_mode, int32_t method, int32_t *d_order_out,
+                                    double *d_coef_out, double *d_aic_out, void *stream);
+
 /* ---- synthetic workload generator (ARIMAModel.sample semantics, ARIMA.scala:655-678) ---------------- *
  * Writes N x T series (row stride ld) into device memory: per-series coefficients = base +/- U(0, jitter)
  * (redrawn until stationary and invertible), Philox4x32-10 + Box-Muller N(0,1) noise keyed by (seed,

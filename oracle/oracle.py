@@ -235,3 +235,32 @@ def is_invertible(coef, p, q, intercept):
 
 def model_flags(coef, p, q, intercept):
     return (1 if is_stationary(coef, p, q, intercept) else 0) | (2 if is_invertible(coef, p, q, intercept) else 0)
+
+
+def order_search(series, max_p=5, max_d=2, max_q=5, intercept_mode=2, method=0):
+    """Min-approxAIC selection over the (d, p, q, intercept) grid.
+    approxAIC = -2 * logLikelihoodCSS + 2 * (p + q + interceptTerm) (ARIMA.scala:826-830) among fits that
+    returned normally and are stationary and invertible (ARIMA.scala:342); ties keep the first candidate in
+    (d, p, q, intercept) order. Returns (order N x 4, coef N x 11, aic N) like arima_order_search_batch."""
+    series = np.ascontiguousarray(np.atleast_2d(series), dtype=np.float64)
+    N = series.shape[0]
+    order = np.full((N, 4), -1, dtype=np.int32)
+    coef_best = np.full((N, 11), np.nan)
+    aic_best = np.full(N, np.inf)
+    i_vals = {0: [0], 1: [1], 2: [0, 1]}[intercept_mode]
+    for d in range(max_d + 1):
+        for p in range(max_p + 1):
+            for q in range(max_q + 1):
+                for I in i_vals:
+                    k = p + q + I
+                    st, coef, ll, _ = fit_batch(series, p, d, q, I, method)
+                    for i in range(N):
+                        if st[i] != 0 or model_flags(coef[i], p, q, I) != 3:
+                            continue
+                        aic = -2.0 * ll[i] + float(2 * k)
+                        if aic < aic_best[i]:
+                            aic_best[i] = aic
+                            order[i] = (p, d, q, I)
+                            coef_best[i] = 0.0
+                            coef_best[i, :k] = coef[i, :k]
+    return order, coef_best, aic_best

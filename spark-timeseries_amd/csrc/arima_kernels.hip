@@ -232,6 +232,64 @@ __global__ __launch_bounds__(256) void k_forecast(const double *__restrict__ ts_
 }
 
 // =======================================================================================================
+// Order search: keep, per series, the min-approxAIC model among the fits
+// that succeeded and are stationary and invertible (the filter of ARIMA.autoFit, ARIMA.scala:342).
+// approxAIC (ARIMA.scala:826-830) = -2 * logLikelihoodCSS(ts) + 2 * (p + q + interceptTerm), the second term
+// an Int. Candidates arrive in (d, p, q, intercept) lexicographic order; strict < keeps the first on ties.
+// =======================================================================================================
+constexpr int kSearchK = 11;   // 1 + 5 + 5
+
+__global__ __launch_bounds__(256) void k_search_init(double *__restrict__ best_aic, int32_t *__restrict__ order,
+                                                     double *__restrict__ coef, int64_t N) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    best_aic[i] = __builtin_inf();
+    for (int j = 0; j < 4; ++j) order[i * 4 + j] = -1;
+    for (int j = 0; j < kSearchK; ++j) coef[i * kSearchK + j] = __builtin_nan("");
+}
+
+__global__ __launch_bounds__(256) void k_search_select(const double *__restrict__ cand_coef,
+                                                       const double *__restrict__ cand_ll,
+                                                       const int32_t *__restrict__ cand_status,
+                                                       const uint8_t *__restrict__ cand_flags, int64_t N, int p,
+                                                       int d, int q, int I, double *__restrict__ best_aic,
+                                                       int32_t *__restrict__ order, double *__restrict__ coef) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    if (cand_status[i] != ARIMA_ST_OK) return;
+    if ((cand_flags[i] & (ARIMA_FLAG_STATIONARY | ARIMA_FLAG_INVERTIBLE)) !=
+        (ARIMA_FLAG_STATIONARY | ARIMA_FLAG_INVERTIBLE))
+        return;
+    const int k = I + p + q;
+    const double aic = -2.0 * cand_ll[i] + (double)(2 * k);
+    if (!(aic < best_aic[i])) return;
+    best_aic[i] = aic;
+    order[i * 4 + 0] = p;
+    order[i * 4 + 1] = d;
+    order[i * 4 + 2] = q;
+    order[i * 4 + 3] = I;
+    for (int j = 0; j < kSearchK; ++j) coef[i * kSearchK + j] = j < k ? cand_coef[i * k + j] : 0.0;
+}
+
+int launch_search_init(double *best_aic, int32_t *order, double *coef, int64_t N, hipStream_t s) {
+    if (N == 0) return ARIMA_OK;
+    hipLaunchKernelGGL(k_search_init, dim3(grid_for(N, 256)), dim3(256), 0, s, best_aic, order, coef, N);
+    STS_CHECK_LAUNCH();
+    return ARIMA_OK;
+}
+
+int launch_search_select(const double *cand_coef, const double *cand_ll, const int32_t *cand_status,
+                         const uint8_t *cand_flags, int64_t N, int p, int d, int q, int I, double *best_aic,
+                         int32_t *order, double *coef, hipStream_t s) {
+    if (N == 0) return ARIMA_OK;
+    if (I + p + q > kSearchK) return ARIMA_E_UNSUPPORTED;
+    hipLaunchKernelGGL(k_search_select, dim3(grid_for(N, 256)), dim3(256), 0, s, cand_coef, cand_ll, cand_status,
+                       cand_flags, N, p, d, q, I, best_aic, order, coef);
+    STS_CHECK_LAUNCH();
+    return ARIMA_OK;
+}
+
+// =======================================================================================================
 // Synthetic generator: ARIMAModel.sample (ARIMA.scala:655-678) with per-series jittered coefficients
 // =======================================================================================================
 constexpr int kSampleMaxOrder = 8;

@@ -61,6 +61,8 @@ struct arima_handle {
     DevBuf diff, init, hr_status, ctl;
     // host-API staging
     DevBuf h_series, h_coef, h_ll, h_status, h_neval, h_ngrad, h_flags, h_uinit, h_aux;
+    // order-search candidate buffers (one fit of the grid at a time) + host-API staging of its outputs
+    DevBuf os_coef, os_ll, os_status, os_neval, os_ngrad, os_flags, os_order;
     unsigned long long *ctl_host = nullptr;   // pinned
 };
 
@@ -500,6 +502,84 @@ int arima_forecast_batch(arima_handle *h, const double *series, int64_t N, int32
     RCCHK(h, sts::launch_forecast(h->h_series.as<double>(), T, h->h_coef.as<double>(), k, h->h_aux.as<double>(), L, N,
                                   T, p, d, q, I, n_future, s), "forecast");
     if (L > 0) HIPCHK(h, hipMemcpyAsync(out, h->h_aux.ptr, (size_t)N * L * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    return ARIMA_OK;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// order search over (d, p, q, intercept) — SURVEY.md 8(f) row 2 (config C5)
+// ---------------------------------------------------------------------------------------------------------
+static int order_search_locked(arima_handle *h, const double *d_series, int64_t N, int32_t T, int64_t ld,
+                               int32_t max_p, int32_t max_d, int32_t max_q, int32_t intercept_mode, int32_t method,
+                               int32_t *d_order, double *d_coef, double *d_aic, int64_t *n_fits, hipStream_t s) {
+    if (max_p < 0 || max_q < 0 || max_d < 0 || intercept_mode < 0 || intercept_mode > 2)
+        return set_err(h, ARIMA_E_INVALID_ARG, "bad search bounds");
+    if (max_p > 5 || max_q > 5 || max_d > 16) return set_err(h, ARIMA_E_UNSUPPORTED, "p, q <= 5, d <= 16");
+    if (N < 0 || T < 0 || ld < T || !d_order || !d_coef || !d_aic) return set_err(h, ARIMA_E_INVALID_ARG, "bad shape");
+    if (N == 0) return ARIMA_OK;
+    HIPCHK(h, hipSetDevice(h->device));
+    RCCHK(h, h->os_coef.ensure((size_t)N * 11 * sizeof(double)), "workspace");
+    RCCHK(h, h->os_ll.ensure((size_t)N * sizeof(double)), "workspace");
+    RCCHK(h, h->os_status.ensure((size_t)N * sizeof(int32_t)), "workspace");
+    RCCHK(h, h->os_neval.ensure((size_t)N * sizeof(int32_t)), "workspace");
+    RCCHK(h, h->os_ngrad.ensure((size_t)N * sizeof(int32_t)), "workspace");
+    RCCHK(h, h->os_flags.ensure((size_t)N), "workspace");
+    RCCHK(h, sts::launch_search_init(d_aic, d_order, d_coef, N, s), "search_init");
+    const int i_lo = intercept_mode == 1 ? 1 : 0, i_hi = intercept_mode == 0 ? 0 : 1;
+    int64_t fits = 0;
+    for (int d = 0; d <= max_d; ++d)
+        for (int p = 0; p <= max_p; ++p)
+            for (int q = 0; q <= max_q; ++q)
+                for (int I = i_lo; I <= i_hi; ++I) {
+                    // ARIMA(0,d,0) without intercept has no parameters: the reference throws (NoDataException);
+                    // fit_device_locked reports it per series and the select step skips it.
+                    int rc = fit_device_locked(h, d_series, N, T, ld, p, d, q, I, method, nullptr,
+                                               h->os_coef.as<double>(), h->os_ll.as<double>(),
+                                               h->os_status.as<int32_t>(), h->os_neval.as<int32_t>(),
+                                               h->os_ngrad.as<int32_t>(), h->os_flags.as<uint8_t>(), s);
+                    if (rc != ARIMA_OK) return rc;
+                    RCCHK(h, sts::launch_search_select(h->os_coef.as<double>(), h->os_ll.as<double>(),
+                                                       h->os_status.as<int32_t>(), h->os_flags.as<uint8_t>(), N, p,
+                                                       d, q, I, d_aic, d_order, d_coef, s),
+                          "search_select");
+                    ++fits;
+                }
+    if (n_fits) *n_fits = fits;
+    return ARIMA_OK;
+}
+
+int arima_order_search_batch_device(arima_handle *h, const double *d_series, int64_t n_series, int32_t T,
+                                    int64_t ld, int32_t max_p, int32_t max_d, int32_t max_q,
+                                    int32_t intercept_mode, int32_t method, int32_t *d_order_out,
+                                    double *d_coef_out, double *d_aic_out, void *stream) {
+    if (!h) return ARIMA_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    return order_search_locked(h, d_series, n_series, T, ld, max_p, max_d, max_q, intercept_mode, method,
+                               d_order_out, d_coef_out, d_aic_out, nullptr, s);
+}
+
+int arima_order_search_batch(arima_handle *h, const double *series, int64_t N, int32_t T, int32_t max_p,
+                             int32_t max_d, int32_t max_q, int32_t intercept_mode, int32_t method,
+                             int32_t *order_out, double *coef_out, double *aic_out) {
+    if (!h) return ARIMA_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (N < 0 || T < 0) return set_err(h, ARIMA_E_INVALID_ARG, "bad shape");
+    if (N == 0) return ARIMA_OK;
+    if (!series || !order_out || !coef_out || !aic_out) return set_err(h, ARIMA_E_INVALID_ARG, "null buffer");
+    HIPCHK(h, hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    RCCHK(h, h->h_series.ensure((size_t)N * std::max(T, 1) * sizeof(double)), "staging");
+    RCCHK(h, h->h_aux.ensure((size_t)N * 11 * sizeof(double)), "staging");
+    RCCHK(h, h->h_ll.ensure((size_t)N * sizeof(double)), "staging");
+    RCCHK(h, h->os_order.ensure((size_t)N * 4 * sizeof(int32_t)), "staging");
+    if (T > 0) HIPCHK(h, hipMemcpyAsync(h->h_series.ptr, series, (size_t)N * T * sizeof(double), hipMemcpyHostToDevice, s));
+    int rc = order_search_locked(h, h->h_series.as<double>(), N, T, T, max_p, max_d, max_q, intercept_mode, method,
+                                 h->os_order.as<int32_t>(), h->h_aux.as<double>(), h->h_ll.as<double>(), nullptr, s);
+    if (rc != ARIMA_OK) return rc;
+    HIPCHK(h, hipMemcpyAsync(order_out, h->os_order.ptr, (size_t)N * 4 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipMemcpyAsync(coef_out, h->h_aux.ptr, (size_t)N * 11 * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipMemcpyAsync(aic_out, h->h_ll.ptr, (size_t)N * sizeof(double), hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipStreamSynchronize(s));
     return ARIMA_OK;
 }

@@ -43,7 +43,7 @@ EXPORTED = [
     "arima_get_last_stats", "arima_set_option", "arima_fit_batch", "arima_fit_batch_device",
     "arima_difference_batch", "arima_inverse_difference_batch", "arima_css_loglik_batch",
     "arima_css_gradient_batch", "arima_hannan_rissanen_batch", "arima_forecast_batch", "arima_model_flags_batch",
-    "arima_sample_batch_device",
+    "arima_sample_batch_device", "arima_order_search_batch", "arima_order_search_batch_device",
 ]
 
 
@@ -119,6 +119,9 @@ def load():
         L.arima_model_flags_batch.argtypes = [H, _dp, _i64, _i32, _i32, _i32, _u8p]
         L.arima_sample_batch_device.argtypes = [H, _vp, _i64, _i32, _i64, _i32, _i32, _i32, _i32, _dp, _f64, _u64,
                                                 _i64, _vp]
+        L.arima_order_search_batch.argtypes = [H, _dp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32p, _dp, _dp]
+        L.arima_order_search_batch_device.argtypes = [H, _vp, _i64, _i32, _i64, _i32, _i32, _i32, _i32, _i32, _vp,
+                                                      _vp, _vp, _vp]
         _lib = L
         return L
 
@@ -260,6 +263,19 @@ class Engine:
         self._check(self.L.arima_forecast_batch(self.h, _ptr(series), N, T, p, d, q, int(bool(include_intercept)),
                                                 _ptr(coef), n_future, _ptr(out)), "arima_forecast_batch")
         return out
+
+    def order_search(self, series, max_p=5, max_d=2, max_q=5, intercept_mode=2, method=METHOD_CSS_CGD):
+        """Min-approxAIC model over the (d, p, q, intercept) grid per series (see include/sparkts_arima.h).
+        Returns order (N x 4: p, d, q, intercept; -1 when nothing qualified), coef (N x 11), aic (N)."""
+        series = np.ascontiguousarray(np.atleast_2d(series), dtype=np.float64)
+        N, T = series.shape
+        order = np.empty((N, 4), dtype=np.int32)
+        coef = np.empty((N, 11))
+        aic = np.empty(N)
+        self._check(self.L.arima_order_search_batch(self.h, _ptr(series), N, T, max_p, max_d, max_q, intercept_mode,
+                                                    method, _ptr(order, _i32p), _ptr(coef), _ptr(aic)),
+                    "arima_order_search_batch")
+        return order, coef, aic
 
     def model_flags(self, coef, p, q, include_intercept):
         k = p + q + (1 if include_intercept else 0)

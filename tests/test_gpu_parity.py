@@ -248,3 +248,21 @@ def test_forecast_of_fitted_model(engine):
     fc = m.forecast(arr["series"][0], 10)
     mean = arr["series"][0].sum() / arr["series"][0].size
     assert np.all(np.abs(np.ravel(fc)[-10:] - mean) < 1e-4)
+
+
+# ---- order search: same selection as the oracle's grid, bit for bit ----
+@pytest.mark.parametrize("grid", [(5, 2, 5, 2), (2, 1, 2, 1), (3, 0, 1, 0)])
+def test_order_search_matches_oracle(engine, grid):
+    max_p, max_d, max_q, imode = grid
+    N, T = 24, 300
+    s = _device_sample(engine, N, T, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 77).cpu().numpy()
+    s[::5] = O.add_time_dependent_effects(np.random.default_rng(2).standard_normal(T), 1, 0, 1, 1, [3.5, 0.3, 0.7])
+    order, coef, aic = engine.order_search(s, max_p, max_d, max_q, imode)
+    eo, ec, ea = O.order_search(s, max_p, max_d, max_q, imode)
+    assert np.array_equal(order, eo), (order, eo)
+    assert _same(aic, ea)
+    assert _same(coef, ec)
+    if grid == (5, 2, 5, 2):
+        assert np.all(order[:, 0] >= 0)      # the full C5 grid finds a qualifying model for every series
+    else:
+        assert np.any(order[:, 0] >= 0) or max_d == 0
