@@ -27,6 +27,20 @@ CONFIGS = {
 }
 FP64_PEAK_TFLOPS = 78.6    # MI355X fp64 vector peak (spec)
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md)
+# HBM bytes per k_cg_fit launch from the last rocprofv3 PMC passes of this same workload (FETCH_SIZE and
+# WRITE_SIZE in their own runs, gfx950 corrections per MI355X_MICROARCH.md; tools/profile.sh ->
+# tools/summarize_prof.py --traffic). Counters cannot be read inside a timed bench run, so the measured value
+# is carried in this tracked file and reported only when its workload matches the one being run.
+PMC_TRAFFIC_FILE = os.path.join(ROOT, "tools", "pmc_traffic_c2.json")
+
+
+def pmc_traffic(workload):
+    try:
+        with open(PMC_TRAFFIC_FILE) as f:
+            m = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return m if m.get("workload") == workload else None
 SEED = 20261015
 
 
@@ -146,6 +160,7 @@ def main():
     result = None
     if rank == 0:
         total_series = N * world
+        pmc = pmc_traffic({"series": N, "T": T, "p": p, "d": d, "q": q, "I": int(I)})
         result = {
             "metric": "series fitted/sec, ARIMA(2,1,2) CSS-CGD, 1M x 1024 pts" if args.config == "c2"
             else f"series fitted/sec, {args.config}",
@@ -171,7 +186,9 @@ def main():
                                      "cg_fit": s0["ms_cg_fit"]}},
             "roofline": {"bound": "fp64-valu", "kernel": "k_cg_fit", "achieved": achieved_tf,
                          "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved_tf / FP64_PEAK_TFLOPS,
-                         "traffic": None,
+                         "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+                         "traffic_unit": "bytes/launch (HBM read+write, rocprofv3 PMC)",
+                         "traffic_source": pmc["source"] if pmc else None,
                          "traffic_model_GBps": passes_bytes / (cg_ms * 1e-3) / 1e9,
                          "hbm_peak_GBps": HBM_PEAK_GBS},
             "cpu_baseline": None,

@@ -4,7 +4,9 @@ HBM bytes follow MI355X_MICROARCH.md's HBM section: FETCH_SIZE is in KB and repo
 streaming read on gfx950 (so it is doubled here); WRITE_SIZE is taken as is. SQ_WAVE_CYCLES / SQ_WAIT_* /
 SQ_ACTIVE_* count quad-cycles. Values are per launch (counter sum / launches of that kernel in the pass).
 
-usage: python tools/summarize_prof.py gpurun_out [out.txt]
+usage: python tools/summarize_prof.py gpurun_out [out.txt] [--traffic tools/pmc_traffic_c2.json --source NAME]
+(--traffic writes k_cg_fit's measured HBM bytes per launch for bench.py's roofline.traffic; the workload keys
+ are those of bench.py's default C2 run that tools/profile.sh profiles)
 """
 import csv
 import glob
@@ -44,6 +46,17 @@ def counters(root):
 
 
 def main():
+    argv = list(sys.argv)
+    traffic_path = source = None
+    if "--traffic" in argv:
+        i = argv.index("--traffic")
+        traffic_path = argv[i + 1]
+        del argv[i:i + 2]
+    if "--source" in argv:
+        i = argv.index("--source")
+        source = argv[i + 1]
+        del argv[i:i + 2]
+    sys.argv = argv
     root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
     ks = kernel_stats(root)
     cs = counters(root)
@@ -69,6 +82,14 @@ def main():
                 extra = f"  -> HBM write {b / 1e9:.3f} GB/launch"
             lines.append(f"   {name:28s} {mean:18.1f}{extra}")
     txt = "\n".join(lines)
+    fit = cs.get("k_cg_fit<2, 2, 1, false, 4>") or next((v for k, v in cs.items() if k.startswith("k_cg_fit")), {})
+    if traffic_path and "FETCH_SIZE" in fit and "WRITE_SIZE" in fit:
+        import json
+        rd = sum(fit["FETCH_SIZE"]) / len(fit["FETCH_SIZE"]) * 1024 * 2
+        wr = sum(fit["WRITE_SIZE"]) / len(fit["WRITE_SIZE"]) * 1024
+        json.dump({"workload": {"series": 1048576, "T": 1024, "p": 2, "d": 1, "q": 2, "I": 1},
+                   "kernel": "k_cg_fit", "hbm_bytes_per_launch": rd + wr, "read_bytes": rd, "write_bytes": wr,
+                   "source": source or root}, open(traffic_path, "w"), indent=1)
     print(txt)
     if len(sys.argv) > 2:
         open(sys.argv[2], "w").write(txt + "\n")
