@@ -135,6 +135,10 @@ int arima_hannan_rissanen_batch(arima_handle *h, const double *diffed, int64_t n
 int arima_forecast_batch(arima_handle *h, const double *series, int64_t n_series, int32_t T,
                          int32_t p, int32_t d, int32_t q, int32_t include_intercept, const double *coef,
                          int32_t n_future, double *out);
+/* Same, device-resident: d_series N x T (row stride ld), d_coef N x k, d_out N x (T + n_future) (row stride ld_out) */
+int arima_forecast_batch_device(arima_handle *h, const double *d_series, int64_t n_series, int32_t T, int64_t ld,
+                                int32_t p, int32_t d, int32_t q, int32_t include_intercept, const double *d_coef,
+                                int32_t n_future, double *d_out, int64_t ld_out, void *stream);
 /* ARIMAModel.isStationary / isInvertible (ARIMA.scala:777-815) for N coefficient rows, flags_out N */
 int arima_model_flags_batch(arima_handle *h, const double *coef, int64_t n_series, int32_t p, int32_t q,
                             int32_t include_intercept, uint8_t *flags_out);

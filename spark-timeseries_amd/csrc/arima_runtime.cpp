@@ -506,6 +506,23 @@ int arima_forecast_batch(arima_handle *h, const double *series, int64_t N, int32
     return ARIMA_OK;
 }
 
+int arima_forecast_batch_device(arima_handle *h, const double *d_series, int64_t N, int32_t T, int64_t ld,
+                                int32_t p, int32_t d, int32_t q, int32_t I, const double *d_coef, int32_t n_future,
+                                double *d_out, int64_t ld_out, void *stream) {
+    if (!h) return ARIMA_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    RCCHK(h, check_orders(h, p, d, q, I), "orders");
+    if (N < 0 || T < d || n_future < 0 || ld < T || ld_out < (int64_t)T + n_future)
+        return set_err(h, ARIMA_E_INVALID_ARG, "bad shape");
+    if (N == 0) return ARIMA_OK;
+    if (!d_series || !d_coef || !d_out) return set_err(h, ARIMA_E_INVALID_ARG, "null buffer");
+    HIPCHK(h, hipSetDevice(h->device));
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    RCCHK(h, sts::launch_forecast(d_series, ld, d_coef, I + p + q, d_out, ld_out, N, T, p, d, q, I, n_future, s),
+          "forecast");
+    return ARIMA_OK;
+}
+
 // ---------------------------------------------------------------------------------------------------------
 // order search over (d, p, q, intercept) — SURVEY.md 8(f) row 2 (config C5)
 // ---------------------------------------------------------------------------------------------------------

@@ -44,6 +44,7 @@ EXPORTED = [
     "arima_difference_batch", "arima_inverse_difference_batch", "arima_css_loglik_batch",
     "arima_css_gradient_batch", "arima_hannan_rissanen_batch", "arima_forecast_batch", "arima_model_flags_batch",
     "arima_sample_batch_device", "arima_order_search_batch", "arima_order_search_batch_device",
+    "arima_forecast_batch_device",
 ]
 
 
@@ -119,6 +120,8 @@ def load():
         L.arima_model_flags_batch.argtypes = [H, _dp, _i64, _i32, _i32, _i32, _u8p]
         L.arima_sample_batch_device.argtypes = [H, _vp, _i64, _i32, _i64, _i32, _i32, _i32, _i32, _dp, _f64, _u64,
                                                 _i64, _vp]
+        L.arima_forecast_batch_device.argtypes = [H, _vp, _i64, _i32, _i64, _i32, _i32, _i32, _i32, _vp, _i32, _vp,
+                                                  _i64, _vp]
         L.arima_order_search_batch.argtypes = [H, _dp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32p, _dp, _dp]
         L.arima_order_search_batch_device.argtypes = [H, _vp, _i64, _i32, _i64, _i32, _i32, _i32, _i32, _i32, _vp,
                                                       _vp, _vp, _vp]
@@ -263,6 +266,20 @@ class Engine:
         self._check(self.L.arima_forecast_batch(self.h, _ptr(series), N, T, p, d, q, int(bool(include_intercept)),
                                                 _ptr(coef), n_future, _ptr(out)), "arima_forecast_batch")
         return out
+
+    def forecast_device(self, d_series, n_series, T, ld, p, d, q, include_intercept, d_coef, n_future, d_out, ld_out,
+                        stream=None):
+        """Device-pointer forecast (ints = raw HBM addresses)."""
+        self._check(self.L.arima_forecast_batch_device(self.h, d_series, n_series, T, ld, p, d, q,
+                                                       int(bool(include_intercept)), d_coef, n_future, d_out, ld_out,
+                                                       stream), "arima_forecast_batch_device")
+
+    def order_search_device(self, d_series, n_series, T, ld, max_p, max_d, max_q, intercept_mode, d_order, d_coef,
+                            d_aic, method=METHOD_CSS_CGD, stream=None):
+        """Device-pointer order search (ints = raw HBM addresses)."""
+        self._check(self.L.arima_order_search_batch_device(self.h, d_series, n_series, T, ld, max_p, max_d, max_q,
+                                                           intercept_mode, method, d_order, d_coef, d_aic, stream),
+                    "arima_order_search_batch_device")
 
     def order_search(self, series, max_p=5, max_d=2, max_q=5, intercept_mode=2, method=METHOD_CSS_CGD):
         """Min-approxAIC model over the (d, p, q, intercept) grid per series (see include/sparkts_arima.h).
