@@ -28,7 +28,8 @@
  * AutoregressionSuite.scala:26-44, python/sparkts/models/test/test_ARIMA.py:20-64, including the
  * path-dependent user-init test (test_ARIMA.py:27-32). Those tests pin results to tolerances (0.01-0.1), not
  * bit patterns, so bit-level agreement with the JVM is unpinned; the two known ambiguities are
- *   (1) Breeze's overlapping `dEdTheta(1 to -1, ::) := dEdTheta(0 to -2, ::)` (shift vs smear, q >= 2),
+ *   (1) Breeze's overlapping `dEdTheta(1 to -1, ::) := dEdTheta(0 to -2, ::)` (shift vs smear, q >= 2;
+ *       decided for smear from Breeze 0.12's slice and OpSet implementation; shift kept),
  *   (2) HotSpot's Math.log intrinsic vs fdlibm (<= 1 ulp on rare inputs).
  *
  * Numerics: compile with -ffp-contract=off and no -ffast-math (Java never contracts a*b+c into an FMA).
@@ -176,8 +177,12 @@ double orc_loglik_css_arma(const double *y, int n, int p, int q, int I, const do
 }
 
 /* gradientlogLikelihoodCSSARMA  ARIMA.scala:465-534.
- * smear == 0: Breeze copies the overlapping row slice like memmove (row shift, SURVEY default);
- * smear == 1: element-wise ascending copy (every lag row becomes row 0). See SURVEY.md 0-7 / C-7. */
+ * `dEdTheta(1 to -1, ::) := dEdTheta(0 to -2, ::)` (:526) under Breeze 0.12: both slices are
+ * strided views of the same (q+1) x k column-major array (canSliceRows: offset = first row, majorStride =
+ * q + 1); the DenseMatrix OpSet walks columns outer, rows inner ascending, with no overlap check, so row r+1
+ * receives the already overwritten row r:
+ * smear == 1 (default): element-wise ascending copy (every lag row becomes row 0);
+ * smear == 0: memmove-like row shift (what a copy-on-overlap implementation would give). */
 void orc_gradient_css_arma(const double *y, int n, int p, int q, int I, const double *coef, int smear,
                            double *grad) {
     int k = I + p + q;

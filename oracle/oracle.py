@@ -24,6 +24,10 @@ ST_NAMES = {0: "OK", 1: "MAX_EVAL", 2: "BRACKET_MAX_EVAL", 3: "MAX_ITER", 4: "SI
 _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int)
 
+# Breeze 0.12 semantics of the overlapping row-slice copy at ARIMA.scala:526: 1 = element-wise
+# ascending copy (every lag row becomes row 0, "smear"), the default; 0 = memmove-like row shift.
+DEFAULT_SMEAR = 1
+
 
 def build():
     subprocess.check_call(["make", "-s", "-C", _HERE])
@@ -101,7 +105,7 @@ def loglik_css(ts, p, d, q, intercept, coef):
     return loglik_css_arma(differences_of_order_d(ts, d)[d:], p, q, intercept, coef)
 
 
-def gradient_css_arma(diffed, p, q, intercept, coef, smear=0):
+def gradient_css_arma(diffed, p, q, intercept, coef, smear=DEFAULT_SMEAR):
     y, py = _c(diffed)
     c, pc = _c(coef)
     g = np.empty(len(c))
@@ -133,7 +137,7 @@ def hannan_rissanen(diffed, p, q, intercept):
     return st, out[:k]
 
 
-def fit(ts, p, d, q, intercept=True, method=0, user_init=None, smear=0):
+def fit(ts, p, d, q, intercept=True, method=0, user_init=None, smear=DEFAULT_SMEAR):
     """ARIMA.fitModel restated. Returns dict(status, coef, ll, n_eval, n_grad, n_iter)."""
     ts, pt = _c(ts)
     k = p + q + (1 if intercept else 0)
@@ -148,7 +152,7 @@ def fit(ts, p, d, q, intercept=True, method=0, user_init=None, smear=0):
     return dict(status=st, coef=coef[:k], ll=ll.value, n_eval=cnt[0], n_grad=cnt[1], n_iter=cnt[2])
 
 
-def fit_batch(series, p, d, q, intercept=True, method=0, user_init=None, smear=0, threads=None):
+def fit_batch(series, p, d, q, intercept=True, method=0, user_init=None, smear=DEFAULT_SMEAR, threads=None):
     """Batch of fits (OpenMP over series). series: (N, T) float64. Returns (status, coef, ll, counters)."""
     series = np.ascontiguousarray(series, dtype=np.float64)
     N, T = series.shape
@@ -237,7 +241,7 @@ def model_flags(coef, p, q, intercept):
     return (1 if is_stationary(coef, p, q, intercept) else 0) | (2 if is_invertible(coef, p, q, intercept) else 0)
 
 
-def order_search(series, max_p=5, max_d=2, max_q=5, intercept_mode=2, method=0):
+def order_search(series, max_p=5, max_d=2, max_q=5, intercept_mode=2, method=0, smear=DEFAULT_SMEAR):
     """Min-approxAIC selection over the (d, p, q, intercept) grid.
     approxAIC = -2 * logLikelihoodCSS + 2 * (p + q + interceptTerm) (ARIMA.scala:826-830) among fits that
     returned normally and are stationary and invertible (ARIMA.scala:342); ties keep the first candidate in
@@ -253,7 +257,7 @@ def order_search(series, max_p=5, max_d=2, max_q=5, intercept_mode=2, method=0):
             for q in range(max_q + 1):
                 for I in i_vals:
                     k = p + q + I
-                    st, coef, ll, _ = fit_batch(series, p, d, q, I, method)
+                    st, coef, ll, _ = fit_batch(series, p, d, q, I, method, smear=smear)
                     for i in range(N):
                         if st[i] != 0 or model_flags(coef[i], p, q, I) != 3:
                             continue

@@ -53,7 +53,7 @@ struct arima_handle {
     std::mutex mu;
     std::string err;
     arima_fit_stats stats{};
-    int smear = 0;
+    int smear = 1;            // Breeze 0.12 overlap semantics at ARIMA.scala:526: element-wise copy
     int grid_blocks_override = 0;
     int g_permille = 750;     // G-pass deferral (see k_cg_fit); tuned on C2
     int64_t last_grid = 0;

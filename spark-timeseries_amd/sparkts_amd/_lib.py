@@ -37,6 +37,10 @@ METHODS = {"css-cgd": METHOD_CSS_CGD, "css-bobyqa": METHOD_CSS_BOBYQA}
 FLAG_STATIONARY = 1
 FLAG_INVERTIBLE = 2
 
+# arima_set_option("smear", .) default: Breeze 0.12's element-wise copy of the overlapping row slice at
+# ARIMA.scala:526; 0 selects the memmove-like row shift.
+DEFAULT_SMEAR = 1
+
 # every symbol include/sparkts_arima.h declares (checked by tests/test_abi.py)
 EXPORTED = [
     "arima_create", "arima_destroy", "arima_last_error", "arima_status_name", "arima_num_params",

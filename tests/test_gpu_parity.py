@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 
 import oracle as O
+import sparkts_amd._lib as L
 from conftest import all_cases, load_case
 
 pytestmark = pytest.mark.gpu
@@ -51,7 +52,7 @@ def test_golden_fixture(engine, name):
         res = engine.fit_batch(arr["series"], meta["p"], meta["d"], meta["q"], meta["I"], meta["method"],
                                arr.get("user_init"))
     finally:
-        engine.set_option("smear", 0)
+        engine.set_option("smear", L.DEFAULT_SMEAR)
     check_fit(res, arr, name)
 
 
@@ -89,7 +90,7 @@ def test_gradient_bit_exact(engine, pqi, smear):
     try:
         g = engine.css_gradient(y, p, q, I, coef)
     finally:
-        engine.set_option("smear", 0)
+        engine.set_option("smear", L.DEFAULT_SMEAR)
     exp = np.stack([O.gradient_css_arma(y[i], p, q, I, coef[i], smear) for i in range(64)])
     assert _same(g, exp)
 
