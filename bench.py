@@ -1,18 +1,26 @@
 """Headline benchmark: series fitted/sec, ARIMA(2,1,2) CSS-CGD, 1M x 1024 pts per GPU (BASELINE.json configs[1];
-configs[2] is the same workload sharded over N GPUs, weak scaling).
+configs[2] is the same workload over N GPUs).
 
 A step = one arima_fit_batch_device call (the drop-in for ARIMA.fitModel over one partition) over this rank's
-1M device-resident synthetic series: differencing + Hannan-Rissanen init + the full CSS-CGD fit of every
-series. Inputs are generated on the device before timing (ARIMAModel.sample semantics, Philox + Box-Muller,
-seed 20261015, per-series jitter +-0.05 around ARIMASuite's [8.2, 0.2, 0.5, 0.3, 0.1]).
+device-resident synthetic series: differencing + Hannan-Rissanen init + the full CSS-CGD fit of every series.
+Inputs are generated on the device before timing (ARIMAModel.sample semantics, Philox + Box-Muller, seed
+20261015, per-series jitter +-0.05 around ARIMASuite's [8.2, 0.2, 0.5, 0.3, 0.1]).
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under torch.distributed.run (one rank per
-GPU; gloo only for the barrier and the max-over-ranks timing: the path itself has no collective).
+Launch: python bench.py [--gpus N --steps K --warmup W]. With N > 1 and no torch.distributed environment, this
+process starts `torch.distributed.run` with N ranks (one per GPU) as a child before touching any GPU and exits
+with its status; under torch.distributed.run each rank fits its own contiguous series range (no data-path
+collective; gloo carries only the timing barrier and the max-over-ranks reduction).
+  --series S        series per GPU (weak scaling, default 1M: configs[1], and configs[2] read per GPU)
+  --total-series S  fixed total over all GPUs (strong scaling: configs[2] = 8M series sharded over N GPUs)
+  --smear 0|1       Breeze overlap reading at ARIMA.scala:526 (default 1)
+  --dry-run         no GPU: ranks compute their shards and report (tests/test_multirank.py)
 Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -30,8 +38,9 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md)
 # HBM bytes per k_cg_fit launch from the last rocprofv3 PMC passes of this same workload (FETCH_SIZE and
 # WRITE_SIZE in their own runs, gfx950 corrections per MI355X_MICROARCH.md; tools/profile.sh ->
 # tools/summarize_prof.py --traffic). Counters cannot be read inside a timed bench run, so the measured value
-# is carried in this tracked file and reported only when its workload matches the one being run.
+# is carried in this tracked file and reported only when its workload (and build tag) matches the one run.
 PMC_TRAFFIC_FILE = os.path.join(ROOT, "tools", "pmc_traffic_c2.json")
+SEED = 20261015
 
 
 def pmc_traffic(workload):
@@ -41,28 +50,46 @@ def pmc_traffic(workload):
     except (OSError, ValueError):
         return None
     return m if m.get("workload") == workload else None
-SEED = 20261015
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(series_host, p, d, q, I, target_s):
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """Re-run this script under torch.distributed.run with n ranks, as a CHILD process (no exec: nothing here
+    has touched the GPU, and the parent never does). Returns the child's exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def cpu_baseline(series_host, p, d, q, I, smear, target_s):
     """The CPU restatement (oracle/, kind "port") on a bounded sample, OpenMP over this rank's CPU share.
 
     The sample (the first rows of rank 0's shard) is fitted repeatedly until ~target_s seconds have passed."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-    cores = max(1, min(cores, len(os.sched_getaffinity(0)), 64))
+    affinity = len(os.sched_getaffinity(0))
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or affinity
+    cores = max(1, min(cores, affinity, 64))
     os.environ["OMP_NUM_THREADS"] = str(cores)
     O.lib()
     sample = series_host
     done, rounds, conv = 0, 0, 0
     t0 = time.perf_counter()
     while True:
-        st, _, _, _ = O.fit_batch(sample, p, d, q, I)
+        st, _, _, _ = O.fit_batch(sample, p, d, q, I, smear=smear)
         done += len(sample)
         rounds += 1
         conv = int((st == 0).sum())
@@ -70,9 +97,11 @@ def cpu_baseline(series_host, p, d, q, I, target_s):
             break
     dt = time.perf_counter() - t0
     return {"value": done / dt, "unit": "series fitted/sec", "cores": cores, "kind": "port",
+            "host_cpus": os.cpu_count(), "affinity_cpus": affinity,
             "sample": f"{len(sample)} synthetic series of the benchmark workload (first rows of rank 0's shard) "
                       f"fitted {rounds}x in {dt:.1f} s by the C restatement oracle/arima_oracle.c "
-                      f"(OpenMP, {cores} threads; {conv}/{len(sample)} converged); not the spark-ts JVM"}
+                      f"(OpenMP, {cores} threads = this process's CPU affinity; the box reports "
+                      f"{os.cpu_count()} CPUs in all; {conv}/{len(sample)} converged); not the spark-ts JVM"}
 
 
 def main():
@@ -82,35 +111,72 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--series", type=int, default=1 << 20, help="series per GPU (weak scaling)")
+    ap.add_argument("--total-series", type=int, default=0, help="fixed total series over all GPUs (strong scaling)")
+    ap.add_argument("--smear", type=int, default=1, choices=[0, 1])
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (0 = skip)")
     ap.add_argument("--grid-blocks", type=int, default=0)
+    ap.add_argument("--dry-run", action="store_true")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
 
     import numpy as np
     import torch
     import torch.distributed as dist
 
+    from sparkts_amd.sharding import max_over_ranks, shard_range, weak_scaling_range
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if world > 1:
+        if not args.dry_run:
+            torch.cuda.set_device(local)
         # the data path has no collective; gloo (CPU) carries only the timing barrier and max-reduction
-        torch.cuda.set_device(local)
         dist.init_process_group("gloo")
-    dev = torch.device("cuda", local)
+
+    p, d, q, I, T, base, jitter = CONFIGS[args.config]
+    if args.total_series:
+        first, last = shard_range(args.total_series, rank, world)     # strong scaling: fixed total
+        scaling = "strong"
+    else:
+        first, last = weak_scaling_range(args.series, rank)          # weak scaling: fixed per GPU
+        scaling = "weak"
+    N = last - first
+    total_series = args.total_series or args.series * world
+    k = p + q + I
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    if args.dry_run:
+        barrier()
+        shards = [None] * world
+        if world > 1:
+            dist.all_gather_object(shards, (first, last))
+        else:
+            shards = [(first, last)]
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "scaling": scaling, "total_series": total_series,
+                              "shards": shards}), flush=True)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
 
     import sparkts_amd._lib as L
+    dev = torch.device("cuda", local)
     eng = L.Engine.get(local)
+    eng.set_option("smear", args.smear)
     if args.grid_blocks:
         eng.set_option("grid_blocks", args.grid_blocks)
 
-    from sparkts_amd.sharding import max_over_ranks, weak_scaling_range
-    p, d, q, I, T, base, jitter = CONFIGS[args.config]
-    N = args.series
-    first, _ = weak_scaling_range(N, rank)            # contiguous series range of this rank
     series = torch.empty((N, T), dtype=torch.float64, device=dev)
     eng.sample_device(series.data_ptr(), N, T, T, p, d, q, I, base, jitter, SEED, first)
-    k = p + q + I
     coef = torch.empty((N, k), dtype=torch.float64, device=dev)
     ll = torch.empty(N, dtype=torch.float64, device=dev)
     status = torch.empty(N, dtype=torch.int32, device=dev)
@@ -120,47 +186,47 @@ def main():
     torch.cuda.synchronize(dev)
 
     def step():
+        # asynchronous: enqueues difference -> HR init -> CG fit on the handle's stream and returns
         eng.fit_batch_device(series.data_ptr(), N, T, T, p, d, q, I, coef.data_ptr(), ll.data_ptr(),
-                             status.data_ptr(), n_eval.data_ptr(), n_grad.data_ptr(), flags.data_ptr())
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
+                             status.data_ptr(), n_eval.data_ptr(), n_grad.data_ptr(), flags.data_ptr(), blocking=False)
 
     for i in range(args.warmup):
         t0 = time.perf_counter()
         step()
-        log(f"[rank {rank}] warmup {i}: {time.perf_counter() - t0:.3f} s")
-    stats = []
+        s = eng.stats()                   # waits for the step's device work
+        log(f"[rank {rank}] warmup {i}: {time.perf_counter() - t0:.3f} s (cg {s['ms_cg_fit']:.1f} ms)")
     barrier()
+    eng.synchronize()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
         step()
-        stats.append(eng.stats())
-        log(f"[rank {rank}] step {i}: cg {stats[-1]['ms_cg_fit']:.1f} ms, total {stats[-1]['ms_total']:.1f} ms")
+    eng.synchronize()
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0, dist if world > 1 else None)
+    s0 = eng.stats()                      # the last timed step
+    log(f"[rank {rank}] {args.steps} steps in {elapsed:.3f} s; last step: difference {s0['ms_difference']:.1f} ms, "
+        f"hr {s0['ms_hr_init']:.1f} ms, cg {s0['ms_cg_fit']:.1f} ms")
 
     st_h = status.cpu().numpy()
-    conv = float((st_h == 0).mean())
-    s0 = stats[-1]
+    conv = float((st_h == 0).mean()) if N else 1.0
     n = T - d
     M = max(p, q)
     S = n - M
     ff = 2 * (p + q) + 4
     fg = ff + 2 * k * q + 1 + p + q + 2 * k
     cg_flops = s0["f_passes"] * S * ff + s0["g_passes"] * S * fg
-    cg_ms = float(np.mean([s["ms_cg_fit"] for s in stats]))
-    achieved_tf = cg_flops / (cg_ms * 1e-3) / 1e12
-    # HBM bytes actually streamed by the fit kernel: one series row per lane-pass (traffic model)
-    passes_bytes = (s0["f_passes"] + s0["g_passes"]) * n * 8.0
+    cg_ms = s0["ms_cg_fit"]
+    achieved_tf = cg_flops / (cg_ms * 1e-3) / 1e12 if cg_ms > 0 else 0.0
+    wave_passes = s0["wave_f_passes"] + s0["wave_g_passes"] + s0["wave_multi_passes"]
+    served = s0["f_passes"] + s0["g_passes"]
+    lane_util = served / (64.0 * wave_passes) if wave_passes else None
+    # HBM bytes the fit kernel streams by construction: one series row per served lane-pass
+    passes_bytes = served * n * 8.0
 
-    result = None
     if rank == 0:
-        total_series = N * world
-        pmc = pmc_traffic({"series": N, "T": T, "p": p, "d": d, "q": q, "I": int(I)})
+        pmc = pmc_traffic({"series": N, "T": T, "p": p, "d": d, "q": q, "I": int(I), "smear": args.smear})
         result = {
             "metric": "series fitted/sec, ARIMA(2,1,2) CSS-CGD, 1M x 1024 pts" if args.config == "c2"
             else f"series fitted/sec, {args.config}",
@@ -171,31 +237,43 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": f"synthetic: ARIMAModel.sample semantics on device, seed {SEED}, coef jitter +-{jitter}",
-            "config": {"workload": f"ARIMA({p},{d},{q}){'+c' if I else ''} css-cgd, {N} series x {T} pts per GPU "
-                                   f"(BASELINE.json configs[1]/[2])",
-                       "series_per_gpu": N, "series_len": T, "parallelism": f"series-sharded x{world}, no collective",
+            "config": {"workload": f"ARIMA({p},{d},{q}){'+c' if I else ''} css-cgd, "
+                                   + (f"{total_series} series total over {world} GPU(s)" if scaling == "strong"
+                                      else f"{N} series x {T} pts per GPU") + " (BASELINE.json configs[1]/[2])",
+                       "series_per_gpu": N, "series_total": total_series, "series_len": T,
+                       "parallelism": f"series-sharded x{world}, no collective",
+                       "breeze_overlap": "smear" if args.smear else "shift",
                        "converged_fraction": conv,
-                       "mean_n_eval": s0["n_eval"] / N, "mean_n_grad": s0["n_grad"] / N,
-                       "lane_f_passes_per_series": s0["f_passes"] / N,
-                       "lane_g_passes_per_series": s0["g_passes"] / N,
+                       "mean_n_eval": s0["n_eval"] / max(N, 1), "mean_n_grad": s0["n_grad"] / max(N, 1),
+                       "lane_f_passes_per_series": s0["f_passes"] / max(N, 1),
+                       "lane_g_passes_per_series": s0["g_passes"] / max(N, 1),
                        "kernel_ms": {"difference": s0["ms_difference"], "hr_init": s0["ms_hr_init"],
                                      "cg_fit": s0["ms_cg_fit"]}},
             "roofline": {"bound": "fp64-valu", "kernel": "k_cg_fit", "achieved": achieved_tf,
                          "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved_tf / FP64_PEAK_TFLOPS,
+                         "achieved_source": "algorithmic flops (SURVEY.md 8(d): U*S*(2(p+q)+4) + G*S*(...), "
+                                            "U, G counted by the kernel) / HIP-event time of the launch",
                          "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
                          "traffic_unit": "bytes/launch (HBM read+write, rocprofv3 PMC)",
                          "traffic_source": pmc["source"] if pmc else None,
-                         "traffic_model_GBps": passes_bytes / (cg_ms * 1e-3) / 1e9,
-                         "hbm_peak_GBps": HBM_PEAK_GBS},
+                         "hbm_GBps_pmc": (pmc["hbm_bytes_per_launch"] / (cg_ms * 1e-3) / 1e9) if pmc and cg_ms else None,
+                         "hbm_frac_pmc": (pmc["hbm_bytes_per_launch"] / (cg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS)
+                         if pmc and cg_ms else None,
+                         "traffic_model_GBps": passes_bytes / (cg_ms * 1e-3) / 1e9 if cg_ms else None,
+                         "hbm_peak_GBps": HBM_PEAK_GBS,
+                         "lane_utilisation": lane_util,
+                         "spec_hits_per_series": s0["spec_hits"] / max(N, 1),
+                         "wave_passes": {"f": s0["wave_f_passes"], "g": s0["wave_g_passes"],
+                                         "multi": s0["wave_multi_passes"]}},
             "cpu_baseline": None,
         }
         if world == 1 and args.cpu_seconds > 0:
             host = series[: 4096].cpu().numpy()
-            result["cpu_baseline"] = cpu_baseline(host, p, d, q, I, args.cpu_seconds)
+            result["cpu_baseline"] = cpu_baseline(host, p, d, q, I, args.smear, args.cpu_seconds)
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()

@@ -13,7 +13,10 @@
  * Conventions
  *   - Plain C types only. Host-buffer entry points take caller-owned host memory; the library never keeps a
  *     pointer after return. `*_device` entry points take device (HBM) pointers and a hipStream_t passed as
- *     `void*` (NULL = the handle's own stream) and are asynchronous w.r.t. the host.
+ *     `void*` (NULL = the handle's own stream) and are asynchronous w.r.t. the host: they enqueue their work
+ *     and return (results are valid once that stream reaches the call's end). Calls on one handle are also
+ *     ordered on the device whichever streams they use, because they share the handle's workspaces.
+ *     arima_get_last_stats waits for the last call's device work. Host-buffer entry points block.
  *   - A batch is N series of equal length T, series-major: element t of series i is series[i*ld + t]
  *     (ld == T for the host-buffer entry points). One call = one Spark partition bucketed by length.
  *   - Coefficient layout per series is the reference's: [c?, phi_1..phi_p, theta_1..theta_q]
@@ -79,19 +82,21 @@ typedef struct arima_fit_stats {
     int64_t grid_blocks;     /* workgroups of the persistent fit kernel                               */
     int64_t spec_hits;       /* objective evaluations answered by a speculative line-search point     */
     int64_t wave_multi_passes; /* wave-level objective passes that carried speculative points          */
-    int64_t diag[6];         /* diagnostics of builds with -DSTS_TIMING (shader cycles summed over waves:
-                                [0] optimizer state machine, [1] all passes, [2] wave lifetime,
-                                [3] gradient passes, [4] multi-point passes); else 0                  */
+    int64_t spec_chains;     /* objective chains evaluated by lane F passes (primary + speculative)    */
+    int64_t diag[6];         /* diagnostics of builds with -DSTS_TIMING; else 0                       */
 } arima_fit_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------------------- */
-/* One handle per device. Calls on one handle are serialised internally (thread-safe). */
+/* One handle per device. Calls on one handle are serialised internally (thread-safe). arima_get_last_stats
+ * waits for the device work of the last fit on the handle (the fit calls themselves do not). */
 int         arima_create(int device, arima_handle **out);
 int         arima_destroy(arima_handle *h);
 const char *arima_last_error(const arima_handle *h);
 const char *arima_status_name(int status);
 int         arima_num_params(int p, int q, int include_intercept);
 int         arima_get_last_stats(const arima_handle *h, arima_fit_stats *out);
+/* Blocks until the device work of every call issued on the handle so far has finished. */
+int         arima_synchronize(arima_handle *h);
 /* Tuning knob for the in-kernel scheduler (0 = default). Not part of the reference contract. */
 int         arima_set_option(arima_handle *h, const char *name, int64_t value);
 

@@ -13,12 +13,10 @@
 #include <stdint.h>
 
 #include "../../include/sparkts_arima.h"
+#include "cg_lane.hpp"
 
 namespace sts {
 
-constexpr int kMaxEval = 10000;      // new MaxEval(10000)  ARIMA.scala:196
-constexpr int kMaxIter = 10000;      // new MaxIter(10000)  ARIMA.scala:195
-constexpr int kBracketMax = 500;     // commons BracketFinder() = BracketFinder(growLimit 100, maxEval 500)
 constexpr int kChunk = 16;           // doubles per lane per streamed chunk (one 128-B line)
 
 
@@ -89,8 +87,6 @@ __device__ __forceinline__ double css_to_loglik(double css, int n) {
     double sigma2 = css / (double)n;
     return (double)(-n / 2) * dlog(2.0 * 3.141592653589793 * sigma2) - css / (2.0 * sigma2);
 }
-
-__device__ __forceinline__ bool finite(double v) { return __builtin_isfinite(v); }
 
 // ------------------------------------------------------------------------------------------------------
 // Per-lane streaming of one series row. Every lane walks its own row front to back, so a wave touches 64
@@ -185,10 +181,13 @@ __device__ __forceinline__ void css_pass(const double *__restrict__ row, int n,
     double e1 = 0.0, e2 = 0.0, css = 0.0, sigma2 = 0.0;
     const double yh0 = 0.0 + (double)I * c[0];
     const double nd = (double)n;
-    double dE[G ? Q + 1 : 1][KA];         // dEdTheta (:476), row r = d e_{t-r} / d theta
+    // dEdTheta (:476), row r = d e_{t-r} / d theta. Under SMEAR (Breeze's element-wise copy at :526, DESIGN.md
+    // 5.1) rows 1..q always hold the same values (the previous row 0), so two rows carry the whole matrix.
+    constexpr int DER = G ? (SMEAR ? (Q > 0 ? 2 : 1) : Q + 1) : 1;
+    double dE[DER][KA];
     if constexpr (G) {
 #pragma unroll
-        for (int r = 0; r <= Q; ++r)
+        for (int r = 0; r < DER; ++r)
 #pragma unroll
             for (int j = 0; j < KA; ++j) dE[r][j] = 0.0;
     }
@@ -210,7 +209,7 @@ __device__ __forceinline__ void css_pass(const double *__restrict__ row, int n,
 #pragma unroll
             for (int j = 0; j < K; ++j)                               // :492-499
 #pragma unroll
-                for (int kk = 0; kk < Q; ++kk) dE[0][j] = dE[0][j] - c[I + P + kk] * dE[kk + 1][j];
+                for (int kk = 0; kk < Q; ++kk) dE[0][j] = dE[0][j] - c[I + P + kk] * dE[SMEAR ? 1 : kk + 1][j];
             double yh = yh0;                                          // :502
             if constexpr (K > 0) dE[0][0] = dE[0][0] - (double)I;     // :503
 #pragma unroll
@@ -233,10 +232,10 @@ __device__ __forceinline__ void css_pass(const double *__restrict__ row, int n,
 #pragma unroll
             for (int j = 0; j < K; ++j) g[j] = g[j] + dE[0][j] * e;   // :524
             if constexpr (SMEAR) {                                    // :526, ascending element copy
+                if constexpr (Q > 0) {
 #pragma unroll
-                for (int r = 1; r <= Q; ++r)
-#pragma unroll
-                    for (int j = 0; j < KA; ++j) dE[r][j] = dE[r - 1][j];
+                    for (int j = 0; j < KA; ++j) dE[1][j] = dE[0][j];
+                }
             } else {                                                  // :526, memmove-like row shift
 #pragma unroll
                 for (int r = Q; r >= 1; --r)
@@ -567,462 +566,6 @@ __device__ __forceinline__ uint8_t model_flags(const double (&c)[I + P + Q > 0 ?
     if (st) f |= ARIMA_FLAG_STATIONARY;
     if (inv) f |= ARIMA_FLAG_INVERTIBLE;
     return f;
-}
-
-// ------------------------------------------------------------------------------------------------------
-// commons-math3 3.4.1 NonLinearConjugateGradientOptimizer(FLETCHER_REEVES, SimpleValueChecker(1e-7, 1e-7))
-// with LineSearch (BracketFinder + BrentOptimizer(1e-15, MIN_VALUE, SimpleUnivariateValueChecker(1e-8,1e-8)))
-// as a per-lane resumable state machine (ARIMA.scala:174-200). The lane posts one request at a time
-// (objective F or gradient G at `x`); the wave serves all posted requests in one pass over the series.
-//
-// Requests that need no pass (every one of them still counted exactly as the reference counts it):
-//   - F(point) at the top of each CG iteration: equals the line search's best value (same point, same ops)
-//     or, on the first iteration, the objective fused into the G(x0) pass;
-//   - the bracket's f(0) = F(point) when the direction is finite; Brent's f(mid) = the bracket's f at mid;
-//   - any non-finite point: the CSS objective and gradient are NaN (every step multiplies every coefficient).
-// ------------------------------------------------------------------------------------------------------
-enum : int { REQ_NONE = 0, REQ_F = 1, REQ_G = 2 };
-
-// Speculative line-search points. In most line searches the bracket's next points do not depend on function
-// values (BracketFinder's golden extension xC = xB + GOLD(xB - xA), then the grow-limit extrapolation
-// wLim = xB + 100 (xC - xB) while the objective keeps rising), so an objective request in the bracket phase
-// carries up to kSpec predicted alphas. The pass evaluates them as extra chains over the same streamed series
-// (same bytes); their values go into a per-lane cache keyed by the exact alpha bits, consulted before any
-// later evaluation of the same line search. A hit is a point the reference evaluates with the same operations,
-// so results (and evaluation counts) are unchanged; a miss only costs the extra chain's arithmetic.
-#ifndef STS_SPEC
-#define STS_SPEC 1
-#endif
-template <int K>
-constexpr int spec_slots() { return K <= 8 ? STS_SPEC : 0; }   // LDS budget: no speculation at K > 8
-
-enum : int {
-    PC_START = 0, PC_G0, PC_TOP, PC_BR_FA, PC_BR_FB, PC_BR_FC, PC_BR_LOOP, PC_BR_A1, PC_BR_C1,
-    PC_BR_SHIFT_EV, PC_BR_SHIFT, PC_BR_END, PC_BRENT_FX, PC_BRENT_LOOP, PC_BRENT_FU, PC_LS_DONE, PC_G,
-    PC_EVAL, PC_DONE
-};
-
-// Precision.equals(x, y, 1)
-__device__ __forceinline__ bool prec_equals(double x, double y) {
-    const long long xi = __double_as_longlong(x), yi = __double_as_longlong(y);
-    bool eq;
-    if (((xi ^ yi) & (long long)0x8000000000000000ull) == 0) {
-        long long dd = xi - yi;
-        eq = (dd < 0 ? -dd : dd) <= 1;
-    } else {
-        const long long NEG0 = (long long)0x8000000000000000ull;
-        long long dplus, dminus;
-        if (xi < yi) { dplus = yi; dminus = xi - NEG0; } else { dplus = xi; dminus = yi - NEG0; }
-        eq = (dplus > 1) ? false : (dminus <= (1 - dplus));
-    }
-    return eq && !__builtin_isnan(x) && !__builtin_isnan(y);
-}
-
-// SimpleValueChecker.converged: |p-c| <= max(|p|,|c|)*rel || |p-c| <= abs, FastMath.max propagates NaN
-__device__ __forceinline__ bool value_converged(double p, double c, double rel, double abs_) {
-    const double diff = fabs(p - c);
-    const double ap = fabs(p), ac = fabs(c);
-    double size;
-    if (ap > ac) size = ap;
-    else if (ap < ac) size = ac;
-    else if (ap != ac) size = __builtin_nan("");
-    else size = ap;
-    return (diff <= size * rel) || (diff <= abs_);
-}
-
-// One lane's optimizer state, kept compact because it lives in LDS for every lane of the persistent fit kernel
-// and its size sets how many waves share a CU: bracket and Brent fields share storage (they are
-// never live together), the request point is recomputed by the pass from (point, dir, ev_alpha) with the same
-// operations, responses arrive as advance() arguments (registers), counters are 16-bit (all bounded by 10001).
-template <int K, int NS_>
-struct CGLane {
-    static constexpr int NS = NS_;
-    static constexpr int NS1 = NS > 0 ? NS : 1;
-    // optimizer (NonLinearConjugateGradientOptimizer.doOptimize)
-    double point[K], dir[K];
-    double delta, memo_obj, prev_obj;
-    // line search: BracketFinder and BrentOptimizer state (disjoint lifetimes)
-    union {
-        struct { double xA, xB, xC, fA, fB, fC, w, fW; };
-        struct { double a, b, bx, bv, bw, bd, be, fx, fv, fw, u, prev_x, prev_f, cur_x, cur_f, best_x, best_f; };
-    };
-    double ev_alpha;                       // pending objective request: point + ev_alpha * dir
-    // speculation: cache of the current line search, and the predicted alphas of the posted request
-    double sp_alpha[NS1], sp_f[NS1], rq_spec[NS1];
-    uint16_t n_eval, n_grad, iter, bcount, spec_hits;
-    uint8_t pc, status, req, have_prev_obj, have_prev, sp_n, rq_nspec;
-
-    __device__ __forceinline__ void start(const double (&init)[K]) {
-#pragma unroll
-        for (int i = 0; i < K; ++i) point[i] = init[i];
-        pc = PC_START;
-        status = ARIMA_ST_OK;
-        n_eval = n_grad = iter = 0;
-        have_prev_obj = 0;
-        req = REQ_NONE;
-        sp_n = rq_nspec = 0;
-        spec_hits = 0;
-    }
-
-    __device__ __forceinline__ void fail(int st) {
-        status = (uint8_t)st;
-        pc = PC_DONE;
-    }
-
-    __device__ __forceinline__ bool done() const { return pc == PC_DONE; }
-
-    // coefficients of the posted request (the same expression PC_EVAL checks for finiteness)
-    __device__ __forceinline__ void request_point(double (&c)[K]) const {
-        if (req == REQ_G) {
-#pragma unroll
-            for (int i = 0; i < K; ++i) c[i] = point[i];
-        } else {
-#pragma unroll
-            for (int i = 0; i < K; ++i) c[i] = point[i] + ev_alpha * dir[i];
-        }
-    }
-
-    // Run the state machine until a request is posted (req != REQ_NONE) or the fit is finished. fr / gr are
-    // the response to the request served last (objective; and the gradient for a G request).
-    __device__ void advance(double fr, const double (&gr)[K]) {
-        const double GOLD = 1.618034, EPS_MIN = 1e-21, GROW = 100.0;
-        const double GS = 0.5 * (3 - __builtin_sqrt(5.0));   // BrentOptimizer.GOLDEN_SECTION
-        double ev_val = fr;                                   // objective value delivered to the resume point
-        double grad[K];                                       // gradient delivered to PC_G0 / PC_G
-#pragma unroll
-        for (int i = 0; i < K; ++i) grad[i] = gr[i];
-        // eval subroutine (LineSearch's objective): locals of this call, never live across a pass
-        double ev_memo = 0.0;
-        int ev_memo_ok = 0, ev_bracket = 0, ev_ret = PC_DONE;
-        auto eval = [&](double alpha, int bracket, int memo_ok, double memo, int ret) {
-            ev_alpha = alpha;
-            ev_bracket = bracket;
-            ev_memo_ok = memo_ok;
-            ev_memo = memo;
-            ev_ret = ret;
-            pc = PC_EVAL;
-        };
-        for (;;) {
-            switch (pc) {
-            case PC_START:
-                // r = computeObjectiveGradient(point)
-                req = REQ_G;
-                pc = PC_G0;
-                return;
-            case PC_G0: {
-                n_grad++;
-                double dl = 0.0;
-#pragma unroll
-                for (int i = 0; i < K; ++i) {
-                    dir[i] = grad[i];                     // steepestDescent = precondition(r) = r.clone()
-                    dl = dl + grad[i] * dir[i];
-                }
-                delta = dl;
-                memo_obj = ev_val;                        // F(point) fused into the gradient pass
-                pc = PC_TOP;
-                break;
-            }
-            case PC_TOP: {
-                if (iter + 1 > kMaxIter) { fail(ARIMA_ST_MAX_ITER); return; }
-                iter++;
-                if (n_eval + 1 > kMaxEval) { fail(ARIMA_ST_MAX_EVAL); return; }
-                n_eval++;
-                const double objective = memo_obj;
-                const bool conv = have_prev_obj && value_converged(prev_obj, objective, 1e-7, 1e-7);
-                prev_obj = objective;
-                have_prev_obj = 1;
-                if (conv) { pc = PC_DONE; return; }   // status OK; point / prev_obj are the result
-                // line.search(point, searchDirection)
-                sp_n = 0;
-                bcount = 0;
-                xA = 0.0;
-                xB = 1e-8;
-                bool dfin = true;
-#pragma unroll
-                for (int i = 0; i < K; ++i) dfin = dfin && finite(dir[i]);
-                eval(xA, 1, dfin ? 1 : 0, objective, PC_BR_FA);
-                break;
-            }
-            case PC_BR_FA:
-                fA = ev_val;
-                eval(xB, 1, 0, 0.0, PC_BR_FB);
-                break;
-            case PC_BR_FB: {
-                fB = ev_val;
-                if (fA > fB) {
-                    double t = xA; xA = xB; xB = t;
-                    t = fA; fA = fB; fB = t;
-                }
-                xC = xB + GOLD * (xB - xA);
-                eval(xC, 1, 0, 0.0, PC_BR_FC);
-                break;
-            }
-            case PC_BR_FC:
-                fC = ev_val;
-                pc = PC_BR_LOOP;
-                break;
-            case PC_BR_LOOP: {
-                if (!(fC > fB)) { pc = PC_BR_END; break; }
-                const double tmp1 = (xB - xA) * (fB - fC);
-                const double tmp2 = (xB - xC) * (fB - fA);
-                const double val = tmp2 - tmp1;
-                const double denom = fabs(val) < EPS_MIN ? 2 * EPS_MIN : val;
-                w = xB - ((xB - xC) * tmp2 - (xB - xA) * tmp1) / (2 * denom);
-                const double wLim = xB + GROW * (xC - xB);
-                if ((w - xC) * (xB - w) > 0) {
-                    eval(w, 1, 0, 0.0, PC_BR_A1);
-                } else if ((w - wLim) * (wLim - xC) >= 0) {
-                    w = wLim;
-                    eval(w, 1, 0, 0.0, PC_BR_SHIFT_EV);
-                } else if ((w - wLim) * (xC - w) > 0) {
-                    eval(w, 1, 0, 0.0, PC_BR_C1);
-                } else {
-                    w = xC + GOLD * (xC - xB);
-                    eval(w, 1, 0, 0.0, PC_BR_SHIFT_EV);
-                }
-                break;
-            }
-            case PC_BR_A1:
-                fW = ev_val;
-                if (fW > fC) {
-                    xA = xB; xB = w; fA = fB; fB = fW;
-                    pc = PC_BR_END;
-                } else if (fW < fB) {
-                    xC = w; fC = fW;
-                    pc = PC_BR_END;
-                } else {
-                    w = xC + GOLD * (xC - xB);
-                    eval(w, 1, 0, 0.0, PC_BR_SHIFT_EV);
-                }
-                break;
-            case PC_BR_C1:
-                fW = ev_val;
-                if (fW > fC) {
-                    xB = xC; xC = w; w = xC + GOLD * (xC - xB); fB = fC; fC = fW;
-                    eval(w, 1, 0, 0.0, PC_BR_SHIFT_EV);
-                } else {
-                    pc = PC_BR_SHIFT;
-                }
-                break;
-            case PC_BR_SHIFT_EV:
-                fW = ev_val;
-                pc = PC_BR_SHIFT;
-                break;
-            case PC_BR_SHIFT:
-                xA = xB; fA = fB; xB = xC; fB = fC; xC = w; fC = fW;
-                pc = PC_BR_LOOP;
-                break;
-            case PC_BR_END: {
-                // bracket -> Brent (shared storage: read everything needed before writing)
-                double lo = xA, hi = xC;
-                const double mid = xB, fmid = fB;
-                if (lo > hi) { double t = lo; lo = hi; hi = t; }
-                if (lo >= hi || mid < lo || mid > hi) { fail(ARIMA_ST_BAD_INTERVAL); return; }  // SearchInterval
-                if (lo < hi) { a = lo; b = hi; } else { a = hi; b = lo; }
-                bx = bv = bw = mid;
-                bd = be = 0.0;
-                eval(mid, 0, 1, fmid, PC_BRENT_FX);                      // fx = f(mid) (memo: bracket fMid)
-                break;
-            }
-            case PC_BRENT_FX:
-                fx = -ev_val;
-                fv = fw = fx;
-                have_prev = 0;
-                cur_x = bx; cur_f = -fx;
-                best_x = cur_x; best_f = cur_f;
-                pc = PC_BRENT_LOOP;
-                break;
-            case PC_BRENT_LOOP: {
-                const double m = 0.5 * (a + b);
-                const double tol1 = 1e-15 * fabs(bx) + 4.9e-324;
-                const double tol2 = 2 * tol1;
-                if (fabs(bx - m) <= tol2 - 0.5 * (b - a)) {
-                    // return best(best, best(previous, current))
-                    double ix = cur_x, iv = cur_f;
-                    if (have_prev && prev_f >= cur_f) { ix = prev_x; iv = prev_f; }
-                    if (!(best_f >= iv)) { best_x = ix; best_f = iv; }
-                    pc = PC_LS_DONE;
-                    break;
-                }
-                double p = 0, q = 0, r = 0;
-                if (fabs(be) > tol1) {
-                    r = (bx - bw) * (fx - fv);
-                    q = (bx - bv) * (fx - fw);
-                    p = (bx - bv) * q - (bx - bw) * r;
-                    q = 2 * (q - r);
-                    if (q > 0) p = -p; else q = -q;
-                    r = be;
-                    be = bd;
-                    if (p > q * (a - bx) && p < q * (b - bx) && fabs(p) < fabs(0.5 * q * r)) {
-                        bd = p / q;
-                        u = bx + bd;
-                        if (u - a < tol2 || b - u < tol2) bd = (bx <= m) ? tol1 : -tol1;
-                    } else {
-                        be = (bx < m) ? b - bx : a - bx;
-                        bd = GS * be;
-                    }
-                } else {
-                    be = (bx < m) ? b - bx : a - bx;
-                    bd = GS * be;
-                }
-                if (fabs(bd) < tol1) u = (bd >= 0) ? bx + tol1 : bx - tol1;
-                else u = bx + bd;
-                eval(u, 0, 0, 0.0, PC_BRENT_FU);
-                break;
-            }
-            case PC_BRENT_FU: {
-                const double fu = -ev_val;
-                prev_x = cur_x; prev_f = cur_f; have_prev = 1;
-                cur_x = u; cur_f = ev_val;
-                {
-                    double ix = cur_x, iv = cur_f;
-                    if (prev_f >= cur_f) { ix = prev_x; iv = prev_f; }
-                    if (!(best_f >= iv)) { best_x = ix; best_f = iv; }
-                }
-                if (value_converged(prev_f, cur_f, 1e-8, 1e-8)) { pc = PC_LS_DONE; break; }
-                if (fu <= fx) {
-                    if (u < bx) b = bx; else a = bx;
-                    bv = bw; fv = fw; bw = bx; fw = fx; bx = u; fx = fu;
-                } else {
-                    if (u < bx) a = u; else b = u;
-                    if (fu <= fw || prec_equals(bw, bx)) { bv = bw; fv = fw; bw = u; fw = fu; }
-                    else if (fu <= fv || prec_equals(bv, bx) || prec_equals(bv, bw)) { bv = u; fv = fu; }
-                }
-                pc = PC_BRENT_LOOP;
-                break;
-            }
-            case PC_LS_DONE: {
-                // point[i] += step * searchDirection[i]; r = computeObjectiveGradient(point)
-                const double step = best_x;
-                memo_obj = best_f;                    // F(point) == Brent's value at `step`
-                bool pfin = true;
-#pragma unroll
-                for (int i = 0; i < K; ++i) {
-                    point[i] = point[i] + step * dir[i];
-                    pfin = pfin && finite(point[i]);
-                }
-                if (!pfin) {                          // the gradient at a non-finite point is NaN: no pass
-#pragma unroll
-                    for (int i = 0; i < K; ++i) grad[i] = __builtin_nan("");
-                    pc = PC_G;
-                    break;
-                }
-                req = REQ_G;
-                pc = PC_G;
-                return;
-            }
-            case PC_G: {
-                n_grad++;
-                const double deltaOld = delta;
-                double dl = 0.0;
-#pragma unroll
-                for (int i = 0; i < K; ++i) dl = dl + grad[i] * grad[i];
-                delta = dl;
-                const double beta = delta / deltaOld;       // FLETCHER_REEVES
-                if (iter % K == 0 || beta < 0) {
-#pragma unroll
-                    for (int i = 0; i < K; ++i) dir[i] = grad[i];
-                } else {
-#pragma unroll
-                    for (int i = 0; i < K; ++i) dir[i] = grad[i] + beta * dir[i];
-                }
-                pc = PC_TOP;
-                break;
-            }
-            case PC_EVAL: {
-                if (ev_bracket) {
-                    if (bcount + 1 > kBracketMax) { fail(ARIMA_ST_BRACKET_MAX_EVAL); return; }
-                    bcount++;
-                }
-                if (n_eval + 1 > kMaxEval) { fail(ARIMA_ST_MAX_EVAL); return; }
-                n_eval++;
-                if (ev_memo_ok) { ev_val = ev_memo; pc = ev_ret; break; }
-                bool fin = true;
-#pragma unroll
-                for (int i = 0; i < K; ++i) fin = fin && finite(point[i] + ev_alpha * dir[i]);
-                if (!fin) { ev_val = __builtin_nan(""); pc = ev_ret; break; }
-                rq_nspec = 0;
-                if constexpr (NS > 0) {
-                    // (static indexing only: the state never needs scratch)
-                    const long long ab = __double_as_longlong(ev_alpha);
-                    bool hit = false;
-#pragma unroll
-                    for (int s = 0; s < NS; ++s)
-                        if (s < sp_n && __double_as_longlong(sp_alpha[s]) == ab) { ev_val = sp_f[s]; hit = true; }
-                    if (hit) { spec_hits++; pc = ev_ret; break; }
-                    // predict the bracket's next value-independent points (same expressions as above)
-                    double bb = 0.0, cc = 0.0, first = 0.0;
-                    bool chain = true, has_first = false;
-                    switch (ev_ret) {
-                    case PC_BR_FB:                                      // xC if fA <= fB, then the wLim chain
-                        cc = xB + GOLD * (xB - xA);
-                        first = cc;
-                        has_first = true;
-                        bb = xB;
-                        break;
-                    case PC_BR_FC: bb = xB; cc = xC; break;            // wLim chain from (xB, xC)
-                    case PC_BR_SHIFT_EV: bb = xC; cc = w; break;       // the shift makes (xB, xC) = (xC, w)
-                    case PC_BR_A1:                                      // no break: golden extension
-                        first = xC + GOLD * (xC - xB);
-                        has_first = true;
-                        chain = false;
-                        break;
-                    case PC_BR_C1:                                      // fW > fC: golden extension from w
-                        first = w + GOLD * (w - xC);
-                        has_first = true;
-                        chain = false;
-                        break;
-                    default: chain = false; break;
-                    }
-                    int cnt = 0;
-#pragma unroll
-                    for (int h = 0; h < NS; ++h) {
-                        if (h == 0 && has_first) {
-                            rq_spec[h] = first;
-                            cnt++;
-                        } else if (chain) {
-                            const double nx = bb + GROW * (cc - bb);
-                            rq_spec[h] = nx;
-                            bb = cc;
-                            cc = nx;
-                            cnt++;
-                        }
-                    }
-                    rq_nspec = (uint8_t)cnt;
-                }
-                req = REQ_F;
-                pc = (uint8_t)ev_ret;                  // resume point once the response arrives
-                return;
-            }
-            case PC_DONE:
-            default:
-                return;
-            }
-        }
-    }
-};
-
-// LDS slot of one lane's optimizer state: padded to an odd number of 8-byte words so that 64 lanes reading the
-// same field with ds_read_b64 hit distinct bank pairs (stride = 8 * odd bytes; MI355X_MICROARCH.md LDS table).
-template <int K, int NS>
-struct alignas(8) LaneSlot {
-    static constexpr int kWords = (int)((sizeof(CGLane<K, NS>) + 7) / 8);
-    static constexpr int kPadWords = (kWords % 2 == 0) ? 1 : 2;   // total word count odd
-    CGLane<K, NS> s;
-    double pad[kPadWords];
-};
-
-// Waves per workgroup of the fit kernel (one workgroup per CU, 64 lanes per wave): as many as the LDS slots of
-// 64 lanes fit in 160 KiB, at most STS_CG_MAX_WAVES (4 = one per SIMD: measured faster than two per SIMD,
-// which halves the pass's register budget and doubles the in-flight streams per CU).
-#ifndef STS_CG_MAX_WAVES
-#define STS_CG_MAX_WAVES 4
-#endif
-template <int K, int NS>
-constexpr int cg_waves() {
-    constexpr int per_wave = 64 * (int)sizeof(LaneSlot<K, NS>);
-    constexpr int w = 163840 / per_wave;
-    return w > STS_CG_MAX_WAVES ? STS_CG_MAX_WAVES : (w < 1 ? 1 : w);
 }
 
 // ------------------------------------------------------------------------------------------------------

@@ -293,6 +293,9 @@ int launch_search_select(const double *cand_coef, const double *cand_ll, const i
 // Synthetic generator: ARIMAModel.sample (ARIMA.scala:655-678) with per-series jittered coefficients
 // =======================================================================================================
 constexpr int kSampleMaxOrder = 8;
+struct SampleCoef {
+    double c[1 + 2 * kSampleMaxOrder];
+};
 
 __device__ bool sample_roots_ok(const double *poly, int N) {   // runtime-order Schur-Cohn (see model_flags)
     double a[kSampleMaxOrder + 1], b[kSampleMaxOrder + 1];
@@ -308,8 +311,9 @@ __device__ bool sample_roots_ok(const double *poly, int N) {   // runtime-order 
 }
 
 __global__ __launch_bounds__(256) void k_sample(double *__restrict__ out, int64_t ld, int64_t N, int T, int p,
-                                                int d, int q, int I, const double *__restrict__ base,
+                                                int d, int q, int I, const SampleCoef base_arg,
                                                 double jitter, uint64_t seed, int64_t first) {
+    const double *base = base_arg.c;
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
     const uint64_t gsid = (uint64_t)(first + i);
@@ -405,10 +409,12 @@ int launch_forecast(const double *ts, int64_t ld_in, const double *coef, int k, 
     return ARIMA_OK;
 }
 
-int launch_sample(double *out, int64_t ld, int64_t N, int T, int p, int d, int q, int I, const double *base,
+int launch_sample(double *out, int64_t ld, int64_t N, int T, int p, int d, int q, int I, const double *base_host,
                   double jitter, uint64_t seed, int64_t first, hipStream_t s) {
     if (N == 0) return ARIMA_OK;
     if (p > kSampleMaxOrder || q > kSampleMaxOrder) return ARIMA_E_UNSUPPORTED;
+    SampleCoef base{};                          // by value: no host buffer outlives the call
+    for (int j = 0; j < I + p + q; ++j) base.c[j] = base_host[j];
     hipLaunchKernelGGL(k_sample, dim3(grid_for(N, 256)), dim3(256), 0, s, out, ld, N, T, p, d, q, I, base, jitter,
                        seed, first);
     STS_CHECK_LAUNCH();
@@ -460,17 +466,17 @@ int launch_ar_fit(const double *y, int64_t ld, int n, int64_t N, int p, int I, d
 int launch_cg_fit(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, int smear,
                   const double *init, const int32_t *init_status, double *coef_out, double *ll_out,
                   int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
-                  unsigned long long *ctl, int grid_blocks, int g_permille, hipStream_t s) {
+                  unsigned long long *ctl, int grid_blocks, hipStream_t s) {
     if (N == 0) return ARIMA_OK;
 #define C_(PP)                                                                                             \
     launch_cg_fit_P<PP>(y, ld, n, N, q, I, smear, init, init_status, coef_out, ll_out, status_out, n_eval_out, \
-                        n_grad_out, flags_out, ctl, grid_blocks, g_permille, s)
+                        n_grad_out, flags_out, ctl, grid_blocks, s)
     STS_P_SWITCH(C_)
 #undef C_
 }
 
-int cg_fit_occupancy_blocks(int p, int q, int I, int smear) {
-#define C_(PP) cg_fit_occupancy_blocks_P<PP>(q, I, smear)
+int cg_fit_series_per_block(int p, int q, int I) {
+#define C_(PP) cg_fit_series_per_block_P<PP>(q, I)
     STS_P_SWITCH(C_)
 #undef C_
 }

@@ -21,6 +21,9 @@
 
 namespace sts {
 
+template <int V>
+using IC = std::integral_constant<int, V>;
+
 // =======================================================================================================
 // least-squares shape checks (commons validateSampleData / Array2DRowRealMatrix), uniform per batch
 // =======================================================================================================
@@ -134,7 +137,16 @@ __global__ __launch_bounds__(256) void k_ar_fit(const double *__restrict__ y, in
 }
 
 // =======================================================================================================
-// Persistent CSS-CGD fit kernel
+// Persistent CSS-CGD fit kernel (ARIMA.scala:174-200 over a batch)
+//
+// One 256-lane workgroup (4 waves, one per SIMD) per CU. Each wave owns SPW > 64 optimizer SLOTS in LDS (one
+// series each: CGLane state + series id). A wave iteration picks up to 64 slots that posted the SAME kind of
+// request (all objective F, or all gradient G), assigns them to its lanes, runs one pass over each assigned
+// slot's series (a G pass also yields the objective; an F pass evaluates the request's predicted points as extra
+// chains over the same streamed bytes), and lets each lane advance its slot's state machine with the response.
+// Finished slots are refilled from a device work counter (wave-aggregated atomics). Oversubscribing the lanes
+// (SPW/64 slots per lane) keeps the passes homogeneous and full: gradient passes cost several objective passes,
+// and a mixed pass would make objective lanes wait for them.
 // =======================================================================================================
 template <int K>
 __device__ __forceinline__ void write_fit(int64_t sid, int status, const double (&coef)[K], double ll, int n_eval,
@@ -151,201 +163,278 @@ __device__ __forceinline__ void write_fit(int64_t sid, int status, const double 
     if (flags_out) flags_out[sid] = ok ? flags : 0;
 }
 
-// Persistent fit kernel: one workgroup of 64 * WAVES lanes per CU (WAVES = cg_waves<K, NS>(), up to two waves
-// per SIMD). Every lane's optimizer state lives in LDS (LaneSlot), so the registers are free for the pass.
-// Per wave iteration: (1) every lane with a response advances its state machine to its next request (finished
-// lanes write their result and start the next series, whose id and initial point were fetched one series
-// ahead); (2) the wave runs one pass over every served lane's own series. A gradient pass costs several
-// objective passes, so lanes that want G sit out objective-only passes until at least g_permille/1000 of the
-// active lanes want G (or nobody wants F); a G pass also yields the objective, so F lanes are served by it too.
-template <int P, int Q, int I, bool SMEAR, int WAVES>
-__global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void k_cg_fit(
+// speculation policy per parameter count (tests/sim/cglane_sim.cpp measures it: 2 predictions per request and a
+// 4-entry line-search cache remove the bracket's value-independent passes and Brent's first two)
+template <int K>
+constexpr int spec_ns() { return 2; }
+template <int K>
+constexpr int spec_nc() { return 4; }
+
+// One optimizer slot in LDS, padded to an odd number of 8-byte words so that 64 lanes reading the same field of
+// 64 different slots with ds_read_b64 spread over the banks (MI355X_MICROARCH.md LDS table).
+template <int K>
+struct FitSlotCore {
+    CGLane<K, spec_ns<K>(), spec_nc<K>()> s;
+    int64_t sid;                    // series of the slot, -1 = empty
+};
+template <int K>
+struct alignas(8) FitSlot {
+    static constexpr int kWords = (int)((sizeof(FitSlotCore<K>) + 7) / 8);
+    static constexpr int kPadWords = (kWords % 2 == 0) ? 1 : 2;
+    FitSlotCore<K> c;
+    double pad[kPadWords];
+};
+
+constexpr int kFitWaves = 4;                 // waves per workgroup (one per SIMD)
+constexpr int kOldEvals = 128;               // evaluations after which a series is served with priority
+constexpr int kFitLdsBudget = 160 * 1024 - 1024;
+// slots per wave: as many as the LDS holds, at most 2 per lane, a multiple of 8, at least 64
+template <int K>
+constexpr int fit_slots_per_wave() {
+    constexpr int fit = kFitLdsBudget / (kFitWaves * (int)sizeof(FitSlot<K>));
+    constexpr int cap = fit > 128 ? 128 : fit;
+    return (cap / 8) * 8;
+}
+
+template <int P, int Q, int I, bool SMEAR, int SPW>
+__global__ __launch_bounds__(64 * kFitWaves, 1) void k_cg_fit(
     const double *__restrict__ y, int64_t ld, int n, int64_t N, const double *__restrict__ init,
     const int32_t *__restrict__ init_status, double *__restrict__ coef_out, double *__restrict__ ll_out,
     int32_t *__restrict__ status_out, int32_t *__restrict__ n_eval_out, int32_t *__restrict__ n_grad_out,
-    uint8_t *__restrict__ flags_out, unsigned long long *__restrict__ ctl, int g_permille) {
-    // ctl[0] = work counter, ctl[1] = lane F passes, ctl[2] = lane G passes, ctl[3] = wave F-only passes,
-    // ctl[4] = wave G passes, ctl[5] = objective evaluations, ctl[6] = gradient evaluations, ctl[7] = spec
-    // hits, ctl[8] = wave multi-point passes, ctl[10..14] = STS_TIMING diagnostics
+    uint8_t *__restrict__ flags_out, unsigned long long *__restrict__ ctl) {
+    // ctl[0] = work counter, ctl[1] = lane F passes, ctl[2] = lane G passes, ctl[3] = wave F passes (one chain),
+    // ctl[4] = wave G passes, ctl[5] = objective evaluations, ctl[6] = gradient evaluations, ctl[7] = spec hits,
+    // ctl[8] = wave F passes with speculative chains, ctl[9] = speculative chains evaluated
     constexpr int K = I + P + Q;
-    constexpr int NS = spec_slots<K>();
-    __shared__ LaneSlot<K, NS> slots[64 * WAVES];
-    CGLane<K, NS> &L = slots[threadIdx.x].s;
-    int64_t sid = -1;
-    bool idle = false, need_new = true;
-    const double *row = y;
-    unsigned long long lane_f = 0, lane_g = 0, wave_f = 0, wave_g = 0, wave_m = 0, evals = 0, grads = 0, hits = 0;
-    const bool lane0 = (threadIdx.x & 63) == 0;
-    // response of the last served request (registers)
-    double resp_f = 0.0, resp_g[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j) resp_g[j] = 0.0;
-    // next series of this lane, fetched one series ahead (id, then its status and initial point)
-    int64_t nxt = (int64_t)atomicAdd(&ctl[0], 1ull);
-    bool nxt_loaded = false;
-    int nxt_st = ARIMA_ST_OK;
-    double nxt_x0[K];
-    L.req = REQ_NONE;
+    constexpr int NS = spec_ns<K>();
+    constexpr int NJ = (SPW + 63) / 64;      // slot groups: lane l owns slots l, l + 64, ...
+    static_assert(SPW >= 64 && SPW <= 128, "slots per wave");
+    __shared__ FitSlot<K> slots[kFitWaves][SPW];
+    __shared__ int assign[kFitWaves][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    FitSlot<K> *ws = slots[wave];
+    unsigned long long lane_f = 0, lane_g = 0, wave_f = 0, wave_g = 0, wave_m = 0, evals = 0, grads = 0, hits = 0,
+                       chains = 0;
+    unsigned round_no = 0;
+    const bool lane0 = lane == 0;
 #ifdef STS_TIMING
-    unsigned long long t_adv = 0, t_pass = 0, t_g = 0, t_m = 0;
-    int kind = 0;
-    const unsigned long long t_birth = __builtin_amdgcn_s_memtime();
+    // diagnostics build only: shader-clock cycles per phase, summed over waves (ctl[10..13]), the kernel span
+    // (ctl[14] = max end, ctl[15] = min start) and the per-wave time after the batch drained (ctl[16])
+    unsigned long long tm_f = 0, tm_g = 0, tm_adv = 0, tm_sel = 0, tm_drain = 0;
+    const unsigned long long tm_start = __builtin_amdgcn_s_memtime();
+    auto now = [] { return __builtin_amdgcn_s_memtime(); };
 #endif
+
+    // Give the slots of the lanes with need = true a new series (or mark them empty once the batch is drained).
+    // Wave-uniform control flow: every lane calls it. Series whose Hannan-Rissanen init failed are reported
+    // here and skipped.
+    auto refill = [&](int slot, bool need) {
+        for (;;) {
+            const unsigned long long m = __ballot(need);
+            if (m == 0ull) break;
+            const int leader = __ffsll((long long)m) - 1;
+            unsigned long long base = 0;
+            if (lane == leader) base = atomicAdd(&ctl[0], (unsigned long long)__popcll(m));
+            base = __shfl(base, leader);
+            if (need) {
+                const int rank = __popcll(m & ((1ull << lane) - 1ull));
+                const int64_t sid = (int64_t)(base + (unsigned long long)rank);
+                FitSlotCore<K> &S = ws[slot].c;
+                if (sid >= N) {
+#ifdef STS_TIMING
+                    if (tm_drain == 0) tm_drain = __builtin_amdgcn_s_memtime();
+#endif
+                    S.sid = -1;
+                    S.s.req = REQ_NONE;
+                    need = false;
+                } else {
+                    const int st0 = init_status ? init_status[sid] : ARIMA_ST_OK;
+                    if (st0 != ARIMA_ST_OK) {
+                        double nanc[K];
+#pragma unroll
+                        for (int j = 0; j < K; ++j) nanc[j] = __builtin_nan("");
+                        write_fit<K>(sid, st0, nanc, 0.0, 0, 0, 0, coef_out, ll_out, status_out, n_eval_out,
+                                     n_grad_out, flags_out);
+                    } else {
+                        double x0[K], g0[K];
+#pragma unroll
+                        for (int j = 0; j < K; ++j) {
+                            x0[j] = init[sid * K + j];
+                            g0[j] = 0.0;
+                        }
+                        S.sid = sid;
+                        S.s.start(x0);
+                        S.s.advance(0.0, g0);           // posts the first request: G at the initial point
+                        need = false;
+                    }
+                }
+            }
+        }
+    };
+
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const int slot = lane + 64 * j;
+        refill(slot < SPW ? slot : 0, slot < SPW);
+    }
+
     for (;;) {
 #ifdef STS_TIMING
-        const unsigned long long t_a0 = __builtin_amdgcn_s_memtime();
+        const unsigned long long t_a = now();
 #endif
-        if (!nxt_loaded && nxt < N) {                 // prefetch the next series' initial point
-            nxt_st = init_status ? init_status[nxt] : ARIMA_ST_OK;
+        // ---- pick the pass: all-G or all-F, up to 64 slots ----
+        // Long-running series (>= kOldEvals evaluations) set the critical path of the launch, so their requests
+        // choose the pass type and are served first; the other slots are taken in a rotating order (no slot
+        // starves while more than 64 requests of its type are pending).
+        unsigned long long mF[NJ], mG[NJ], mO[NJ];
+        int nF = 0, nG = 0, nOF = 0, nOG = 0;
 #pragma unroll
-            for (int j = 0; j < K; ++j) nxt_x0[j] = init[nxt * K + j];
-            nxt_loaded = true;
-        }
-        // ---- per lane: advance the state machine to its next request (refilling finished lanes) ----
-        while (!idle) {
-            if (need_new) {
-                if (nxt >= N) { idle = true; break; }
-                sid = nxt;
-                const int st0 = nxt_st;
-                double x0[K];
-#pragma unroll
-                for (int j = 0; j < K; ++j) x0[j] = nxt_x0[j];
-                nxt = (int64_t)atomicAdd(&ctl[0], 1ull);
-                nxt_loaded = false;
-                need_new = false;
-                row = y + sid * ld;
-                if (st0 != ARIMA_ST_OK) {
-                    double nanc[K];
-#pragma unroll
-                    for (int j = 0; j < K; ++j) nanc[j] = __builtin_nan("");
-                    write_fit<K>(sid, st0, nanc, 0.0, 0, 0, 0, coef_out, ll_out, status_out, n_eval_out,
-                                 n_grad_out, flags_out);
-                    need_new = true;
-                    if (nxt < N) {                    // (rare) the next one is needed right away
-                        nxt_st = init_status ? init_status[nxt] : ARIMA_ST_OK;
-#pragma unroll
-                        for (int j = 0; j < K; ++j) nxt_x0[j] = init[nxt * K + j];
-                        nxt_loaded = true;
-                    }
-                    continue;
-                }
-                L.start(x0);
+        for (int j = 0; j < NJ; ++j) {
+            const int slot = lane + 64 * j;
+            int r = REQ_NONE;
+            bool old = false;
+            if (slot < SPW && ws[slot].c.sid >= 0) {
+                r = ws[slot].c.s.req;
+                old = ws[slot].c.s.n_eval >= kOldEvals;
             }
-            if (L.req != REQ_NONE) break;        // request still pending (deferred G): nothing to advance
-            L.advance(resp_f, resp_g);
-            if (L.done()) {
-                double pt[K];
-#pragma unroll
-                for (int j = 0; j < K; ++j) pt[j] = L.point[j];
-                write_fit<K>(sid, L.status, pt, L.prev_obj, L.n_eval, L.n_grad,
-                             L.status == ARIMA_ST_OK ? model_flags<P, Q, I>(pt) : (uint8_t)0, coef_out, ll_out,
-                             status_out, n_eval_out, n_grad_out, flags_out);
-                evals += L.n_eval;
-                grads += L.n_grad;
-                hits += L.spec_hits;
-                need_new = true;
-                if (!nxt_loaded && nxt < N) {
-                    nxt_st = init_status ? init_status[nxt] : ARIMA_ST_OK;
-#pragma unroll
-                    for (int j = 0; j < K; ++j) nxt_x0[j] = init[nxt * K + j];
-                    nxt_loaded = true;
-                }
-                continue;
-            }
-            break;
+            mF[j] = __ballot(r == REQ_F);
+            mG[j] = __ballot(r == REQ_G);
+            mO[j] = __ballot(old);
+            nF += __popcll(mF[j]);
+            nG += __popcll(mG[j]);
+            nOF += __popcll(mF[j] & mO[j]);
+            nOG += __popcll(mG[j] & mO[j]);
         }
-        // ---- per wave: one pass serving the posted requests ----
-        const unsigned long long act = __ballot(!idle);
-#ifdef STS_TIMING
-        const unsigned long long t_p0 = __builtin_amdgcn_s_memtime();
-        t_adv += t_p0 - t_a0;
-#endif
-        if (act == 0ull) break;
-        const int req = idle ? REQ_NONE : L.req;
-        const unsigned long long wantG = __ballot(req == REQ_G);
-        const int nG = __popcll(wantG), nA = __popcll(act);
-        const bool anyG = nG > 0 && (nG == nA || nG * 1000 >= g_permille * nA);
-        // lanes not served by this pass stream a shared row (L2-resident) instead of their own
-        const bool served = !idle && (anyG || req == REQ_F);
-        const double *prow = served ? row : y;
+        if (nF + nG == 0) break;                  // batch drained and every slot of this wave finished
+        const bool doG = nOG != nOF ? nOG > nOF : (nG >= 64 || (nF < 64 && nG >= nF));
+        const int rot = (int)(round_no * 37u) & 63;
+        round_no++;
+        int base = 0;
+#pragma unroll
+        for (int tier = 0; tier < 2; ++tier) {
+#pragma unroll
+            for (int jj = 0; jj < NJ; ++jj) {
+                const int j = (jj + (int)round_no) % NJ;
+                unsigned long long m = (doG ? mG[j] : mF[j]) & (tier == 0 ? mO[j] : ~mO[j]);
+                m = (m >> rot) | (rot ? (m << (64 - rot)) : 0ull);          // rotate: lane rot ranks first
+                const int lr = (lane - rot) & 63;
+                if ((m >> lr) & 1ull) {
+                    const int rank = base + __popcll(m & ((1ull << lr) - 1ull));
+                    if (rank < 64) assign[wave][rank] = lane + 64 * j;
+                }
+                base += __popcll(m);
+            }
+        }
+        const int nsel = base < 64 ? base : 64;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const bool served = lane < nsel;
+        const int my = served ? assign[wave][lane] : 0;
+        FitSlotCore<K> &S = ws[my].c;
+        // lanes without a slot stream a shared (L2-resident) row with dummy coefficients: uniform control flow
+        const double *row = served ? y + S.sid * ld : y;
         double c[K], css, g[K];
         if (served) {
-            L.request_point(c);
+            S.s.request_point(c);
         } else {
 #pragma unroll
             for (int j = 0; j < K; ++j) c[j] = 0.0;
         }
-        const int nspec = (served && req == REQ_F) ? L.rq_nspec : 0;
-        const bool anySpec = NS > 0 && !anyG && __ballot(nspec > 0) != 0ull;
-        if (anyG) {
-            css_pass<P, Q, I, true, SMEAR>(prow, n, c, css, g);
-            wave_g += lane0;
+        double resp_f = 0.0;
 #ifdef STS_TIMING
-            kind = 1;
+        const unsigned long long t_b = now();
+        tm_sel += t_b - t_a;
 #endif
-        } else if constexpr (NS > 0) {
-            if (anySpec) {
-                // primary point + the lane's speculative points (lanes with fewer repeat the primary)
-                double cm[NS + 1][K], cssm[NS + 1];
+        if (doG) {
+            css_pass<P, Q, I, true, SMEAR>(row, n, c, css, g);
+            resp_f = css_to_loglik(css, n);
+            wave_g += lane0;
+            lane_g += served;
+        } else {
+            // chains = 1 + the most predictions any served lane posted (wave-uniform)
+            const int nsp = served ? (int)S.s.rq_nspec : 0;
+            int nch = 1;
+#pragma unroll
+            for (int h = 1; h <= NS; ++h)
+                if (__ballot(nsp >= h) != 0ull) nch = h + 1;
+            auto multi = [&](auto NCHc) {
+                constexpr int NCH = decltype(NCHc)::value;
+                double cm[NCH][K], cssm[NCH];
 #pragma unroll
                 for (int j = 0; j < K; ++j) cm[0][j] = c[j];
 #pragma unroll
-                for (int h = 0; h < NS; ++h) {
-                    const bool use = h < nspec;
-                    const double al = use ? L.rq_spec[h] : 0.0;
+                for (int h = 1; h < NCH; ++h) {
+                    if (h <= nsp) {
+                        double cs[K];
+                        S.s.spec_point(h - 1, cs);
 #pragma unroll
-                    for (int j = 0; j < K; ++j) cm[h + 1][j] = use ? L.point[j] + al * L.dir[j] : c[j];
-                }
-                css_pass_multi<P, Q, I, NS + 1>(prow, n, cm, cssm);
-                css = cssm[0];
+                        for (int j = 0; j < K; ++j) cm[h][j] = cs[j];
+                    } else {
 #pragma unroll
-                for (int h = 0; h < NS; ++h) {
-                    if (h < nspec) {
-                        L.sp_alpha[h] = L.rq_spec[h];
-                        L.sp_f[h] = css_to_loglik(cssm[h + 1], n);
+                        for (int j = 0; j < K; ++j) cm[h][j] = c[j];
                     }
                 }
-                if (nspec > 0) L.sp_n = (uint8_t)nspec;
-                wave_m += lane0;
-#ifdef STS_TIMING
-                kind = 2;
-#endif
-            } else {
-                css_pass<P, Q, I, false, SMEAR>(prow, n, c, css, g);
-                wave_f += lane0;
-            }
-        } else {
-            css_pass<P, Q, I, false, SMEAR>(prow, n, c, css, g);
-            wave_f += lane0;
-        }
-        if (served) {
-            resp_f = css_to_loglik(css, n);
-            if (req == REQ_G) {
+                css_pass_multi<P, Q, I, NCH>(row, n, cm, cssm);
+                css = cssm[0];
+                if (served) {
 #pragma unroll
-                for (int j = 0; j < K; ++j) resp_g[j] = g[j];
-                lane_g++;
+                    for (int h = 1; h < NCH; ++h)
+                        if (h <= nsp) S.s.spec_store(h - 1, css_to_loglik(cssm[h], n));
+                }
+            };
+            if constexpr (NS >= 2) {
+                if (nch == 3) multi(IC<3>{});
+                else if (nch == 2) multi(IC<2>{});
+                else multi(IC<1>{});
+            } else if constexpr (NS == 1) {
+                if (nch == 2) multi(IC<2>{});
+                else multi(IC<1>{});
             } else {
-                lane_f++;
+                multi(IC<1>{});
             }
-            L.req = REQ_NONE;
+            resp_f = css_to_loglik(css, n);
+            if (nch > 1) wave_m += lane0; else wave_f += lane0;
+            lane_f += served;
+            chains += served ? (unsigned long long)(1 + nsp) : 0ull;
         }
+        // ---- each lane advances its slot with the response; finished slots are written out and refilled ----
 #ifdef STS_TIMING
-        {
-            const unsigned long long dt = __builtin_amdgcn_s_memtime() - t_p0;
-            t_pass += dt;
-            if (kind == 1) t_g += dt;
-            if (kind == 2) t_m += dt;
-            kind = 0;
+        const unsigned long long t_c = now();
+        if (doG) tm_g += t_c - t_b; else tm_f += t_c - t_b;
+#endif
+        bool need = false;
+        if (served) {
+            S.s.req = REQ_NONE;
+            S.s.advance(resp_f, g);
+            if (S.s.done()) {
+                double pt[K];
+#pragma unroll
+                for (int j = 0; j < K; ++j) pt[j] = S.s.point[j];
+                write_fit<K>(S.sid, S.s.status, pt, S.s.prev_obj, S.s.n_eval, S.s.n_grad,
+                             S.s.status == ARIMA_ST_OK ? model_flags<P, Q, I>(pt) : (uint8_t)0, coef_out, ll_out,
+                             status_out, n_eval_out, n_grad_out, flags_out);
+                evals += S.s.n_eval;
+                grads += S.s.n_grad;
+                hits += S.s.spec_hits;
+                need = true;
+            }
         }
+        refill(my, need);
+#ifdef STS_TIMING
+        tm_adv += now() - t_c;
 #endif
     }
 #ifdef STS_TIMING
     if (lane0) {
-        atomicAdd(&ctl[10], t_adv);
-        atomicAdd(&ctl[11], t_pass);
-        atomicAdd(&ctl[12], __builtin_amdgcn_s_memtime() - t_birth);
-        atomicAdd(&ctl[13], t_g);
-        atomicAdd(&ctl[14], t_m);
+        const unsigned long long tm_end = now();
+        atomicAdd(&ctl[10], tm_f);
+        atomicAdd(&ctl[11], tm_g);
+        atomicAdd(&ctl[12], tm_adv);
+        atomicAdd(&ctl[13], tm_sel);
+        atomicMax(&ctl[14], tm_end);
+        atomicMin(&ctl[15], tm_start);
+        atomicAdd(&ctl[16], tm_drain ? tm_end - tm_drain : 0ull);
     }
 #endif
     atomicAdd(&ctl[1], lane_f);
@@ -353,11 +442,12 @@ __global__ __launch_bounds__(64 * WAVES, (WAVES + 3) / 4) void k_cg_fit(
     if (lane0) {
         atomicAdd(&ctl[3], wave_f);
         atomicAdd(&ctl[4], wave_g);
+        atomicAdd(&ctl[8], wave_m);
     }
     atomicAdd(&ctl[5], evals);
     atomicAdd(&ctl[6], grads);
     atomicAdd(&ctl[7], hits);
-    if (lane0) atomicAdd(&ctl[8], wave_m);
+    atomicAdd(&ctl[9], chains);
 }
 
 // =======================================================================================================
@@ -409,18 +499,15 @@ __global__ __launch_bounds__(256) void k_model_flags(const double *__restrict__ 
 // =======================================================================================================
 // per-P launchers (explicitly instantiated one P per translation unit: arima_inst_p{0..5}.hip)
 // =======================================================================================================
-template <int V>
-using IC = std::integral_constant<int, V>;
-
 #ifdef STS_DEV
-// dev build (make dev): only q = STS_DEV_Q, smear off -- fast compiles for kernel experiments
+// dev build (make dev): only q = STS_DEV_Q and the default Breeze reading (smear) -- fast kernel experiments
 template <class Fn>
 int with_order(int v, Fn &&fn) {
     return v == STS_DEV_Q ? fn(IC<STS_DEV_Q>{}) : ARIMA_E_UNSUPPORTED;
 }
 template <class Fn>
 int with_smear(int v, Fn &&fn) {
-    return v ? ARIMA_E_UNSUPPORTED : fn(IC<0>{});
+    return v ? fn(IC<1>{}) : ARIMA_E_UNSUPPORTED;
 }
 #else
 template <class Fn>
@@ -490,7 +577,7 @@ template <int P>
 int launch_cg_fit_P(const double *y, int64_t ld, int n, int64_t N, int q, int I, int smear, const double *init,
                     const int32_t *init_status, double *coef_out, double *ll_out, int32_t *status_out,
                     int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out, unsigned long long *ctl,
-                    int grid_blocks, int g_permille, hipStream_t s) {
+                    int grid_blocks, hipStream_t s) {
     return with_order(q, [&](auto Qc) {
         return with_bool(I, [&](auto Ic) {
             return with_smear(smear, [&](auto Sc) {
@@ -499,10 +586,10 @@ int launch_cg_fit_P(const double *y, int64_t ld, int n, int64_t N, int q, int I,
                 if constexpr (P + Q + II == 0) {
                     return ARIMA_E_INVALID_ARG;
                 } else {
-                    constexpr int W = cg_waves<P + Q + II, spec_slots<P + Q + II>()>();
-                    hipLaunchKernelGGL((k_cg_fit<P, Q, II, S, W>), dim3(grid_blocks), dim3(64 * W), 0, s, y, ld, n, N,
-                                       init, init_status, coef_out, ll_out, status_out, n_eval_out, n_grad_out,
-                                       flags_out, ctl, g_permille);
+                    constexpr int SPW = fit_slots_per_wave<P + Q + II>();
+                    hipLaunchKernelGGL((k_cg_fit<P, Q, II, S, SPW>), dim3(grid_blocks), dim3(64 * kFitWaves), 0, s,
+                                       y, ld, n, N, init, init_status, coef_out, ll_out, status_out, n_eval_out,
+                                       n_grad_out, flags_out, ctl);
                     STS_CHECK_LAUNCH();
                     return ARIMA_OK;
                 }
@@ -511,23 +598,16 @@ int launch_cg_fit_P(const double *y, int64_t ld, int n, int64_t N, int q, int I,
     });
 }
 
+// series one workgroup keeps in flight (blocks of the grid are sized from it)
 template <int P>
-int cg_fit_occupancy_blocks_P(int q, int I, int smear) {
-    int blocks = 0;
-    with_order(q, [&](auto Qc) {
+int cg_fit_series_per_block_P(int q, int I) {
+    return with_order(q, [&](auto Qc) {
         return with_bool(I, [&](auto Ic) {
-            return with_smear(smear, [&](auto Sc) {
-                constexpr int Q = decltype(Qc)::value, II = decltype(Ic)::value;
-                constexpr bool S = decltype(Sc)::value != 0;
-                if constexpr (P + Q + II > 0) {
-                    constexpr int W = cg_waves<P + Q + II, spec_slots<P + Q + II>()>();
-                    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks, k_cg_fit<P, Q, II, S, W>, 64 * W, 0);
-                }
-                return 0;
-            });
+            constexpr int Q = decltype(Qc)::value, II = decltype(Ic)::value;
+            if constexpr (P + Q + II == 0) return 0;
+            else return kFitWaves * fit_slots_per_wave<P + Q + II>();
         });
     });
-    return blocks;
 }
 
 template <int P>
@@ -580,8 +660,8 @@ int launch_model_flags_P(const double *coef, int64_t N, int q, int I, uint8_t *f
                                          int32_t *, int32_t *, int32_t *, uint8_t *, hipStream_t);              \
     EXT template int launch_cg_fit_P<PP>(const double *, int64_t, int, int64_t, int, int, int, const double *,   \
                                          const int32_t *, double *, double *, int32_t *, int32_t *, int32_t *,  \
-                                         uint8_t *, unsigned long long *, int, int, hipStream_t);                \
-    EXT template int cg_fit_occupancy_blocks_P<PP>(int, int, int);                                              \
+                                         uint8_t *, unsigned long long *, int, hipStream_t);                     \
+    EXT template int cg_fit_series_per_block_P<PP>(int, int);                                                   \
     EXT template int launch_css_loglik_P<PP>(const double *, int64_t, int, int64_t, int, int, const double *,    \
                                              double *, hipStream_t);                                            \
     EXT template int launch_css_grad_P<PP>(const double *, int64_t, int, int64_t, int, int, int, const double *, \

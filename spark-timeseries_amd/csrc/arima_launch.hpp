@@ -24,15 +24,16 @@ int launch_ar_fit(const double *y, int64_t ld, int n, int64_t N, int p, int I, d
 int launch_cg_fit(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, int smear,
                   const double *init, const int32_t *init_status, double *coef_out, double *ll_out,
                   int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
-                  unsigned long long *ctl, int grid_blocks, int g_permille, hipStream_t s);
+                  unsigned long long *ctl, int grid_blocks, hipStream_t s);
 int launch_css_loglik(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, const double *coef,
                       double *ll_out, hipStream_t s);
 int launch_css_grad(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, int smear,
                     const double *coef, double *g_out, hipStream_t s);
 int launch_model_flags(const double *coef, int64_t N, int p, int q, int I, uint8_t *flags_out, hipStream_t s);
-int launch_sample(double *out, int64_t ld, int64_t N, int T, int p, int d, int q, int I, const double *base,
+// base_host: I + p + q host doubles (passed to the kernel by value)
+int launch_sample(double *out, int64_t ld, int64_t N, int T, int p, int d, int q, int I, const double *base_host,
                   double jitter, uint64_t seed, int64_t first, hipStream_t s);
-int cg_fit_occupancy_blocks(int p, int q, int I, int smear);
+int cg_fit_series_per_block(int p, int q, int I);   // optimizer slots of one k_cg_fit workgroup
 
 int hr_shape_status_host(int n, int p, int q, int I);
 int ar_shape_status_host(int n, int p, int I);

@@ -22,6 +22,10 @@ namespace {
 struct DevBuf {
     void *ptr = nullptr;
     size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { release(); }
     int ensure(size_t need) {
         if (need <= bytes) return ARIMA_OK;
         if (ptr) hipFree(ptr);
@@ -42,6 +46,18 @@ struct DevBuf {
 };
 
 constexpr int kNumEvents = 5;
+constexpr int kCtlWords = 32;     // device counters of the fit kernel (k_cg_fit's ctl[])
+
+// What arima_get_last_stats needs to turn the device counters of the last fit into arima_fit_stats. The fit
+// entry points do not wait for the device (the `*_device` contract): the counters are copied to pinned host
+// memory in stream order and the stats are computed when they are asked for.
+struct PendingStats {
+    bool valid = false;
+    int64_t N = 0;
+    int n = 0, p = 0, q = 0, I = 0;
+    bool ar_only = false, user_init = false, cg = false;
+    int64_t grid = 0;
+};
 
 }  // namespace
 
@@ -50,12 +66,14 @@ struct arima_handle {
     int num_cus = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[kNumEvents] = {};
-    std::mutex mu;
+    hipEvent_t ev_done = nullptr;     // end of the last call's device work (serialises workspace reuse across streams)
+    bool has_done = false;
+    mutable std::mutex mu;
     std::string err;
     arima_fit_stats stats{};
+    PendingStats pending;
     int smear = 1;            // Breeze 0.12 overlap semantics at ARIMA.scala:526: element-wise copy
     int grid_blocks_override = 0;
-    int g_permille = 750;     // G-pass deferral (see k_cg_fit); tuned on C2
     int64_t last_grid = 0;
     // device workspaces
     DevBuf diff, init, hr_status, ctl;
@@ -143,15 +161,20 @@ int arima_create(int device, arima_handle **out) {
     *out = nullptr;
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ARIMA_E_DEVICE;
+    if (hipSetDevice(device) != hipSuccess) return ARIMA_E_DEVICE;
     arima_handle *h = new arima_handle();
     h->device = device;
-    if (hipSetDevice(device) != hipSuccess) { delete h; return ARIMA_E_DEVICE; }
     hipDeviceGetAttribute(&h->num_cus, hipDeviceAttributeMultiprocessorCount, device);
-    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) { delete h; return ARIMA_E_DEVICE; }
-    for (auto &e : h->ev) hipEventCreate(&e);
-    if (hipHostMalloc((void **)&h->ctl_host, 16 * sizeof(unsigned long long), 0) != hipSuccess) {
-        delete h;
-        return ARIMA_E_OOM;
+    int rc = ARIMA_OK;
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) rc = ARIMA_E_DEVICE;
+    for (auto &e : h->ev)
+        if (rc == ARIMA_OK && hipEventCreate(&e) != hipSuccess) rc = ARIMA_E_DEVICE;
+    if (rc == ARIMA_OK && hipEventCreateWithFlags(&h->ev_done, hipEventDisableTiming) != hipSuccess) rc = ARIMA_E_DEVICE;
+    if (rc == ARIMA_OK && hipHostMalloc((void **)&h->ctl_host, kCtlWords * sizeof(unsigned long long), 0) != hipSuccess)
+        rc = ARIMA_E_OOM;
+    if (rc != ARIMA_OK) {
+        arima_destroy(h);
+        return rc;
     }
     *out = h;
     return ARIMA_OK;
@@ -160,22 +183,39 @@ int arima_create(int device, arima_handle **out) {
 int arima_destroy(arima_handle *h) {
     if (!h) return ARIMA_E_INVALID_ARG;
     hipSetDevice(h->device);
-    hipStreamSynchronize(h->stream);
-    for (DevBuf *b : {&h->diff, &h->init, &h->hr_status, &h->ctl, &h->h_series, &h->h_coef, &h->h_ll,
-                      &h->h_status, &h->h_neval, &h->h_ngrad, &h->h_flags, &h->h_uinit, &h->h_aux})
-        b->release();
-    for (auto &e : h->ev) hipEventDestroy(e);
+    if (h->stream) hipStreamSynchronize(h->stream);
+    if (h->has_done) hipEventSynchronize(h->ev_done);
+    for (auto &e : h->ev)
+        if (e) hipEventDestroy(e);
+    if (h->ev_done) hipEventDestroy(h->ev_done);
     if (h->ctl_host) hipHostFree(h->ctl_host);
-    hipStreamDestroy(h->stream);
-    delete h;
+    if (h->stream) hipStreamDestroy(h->stream);
+    delete h;                                  // every DevBuf workspace frees itself
     return ARIMA_OK;
 }
 
 const char *arima_last_error(const arima_handle *h) { return h ? h->err.c_str() : "null handle"; }
 
-int arima_get_last_stats(const arima_handle *h, arima_fit_stats *out) {
-    if (!h || !out) return ARIMA_E_INVALID_ARG;
+static void finish_stats(arima_handle *h);
+
+int arima_get_last_stats(const arima_handle *hc, arima_fit_stats *out) {
+    if (!hc || !out) return ARIMA_E_INVALID_ARG;
+    arima_handle *h = const_cast<arima_handle *>(hc);   // the lazy completion below only fills h->stats
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (h->pending.valid) {
+        hipSetDevice(h->device);
+        if (hipEventSynchronize(h->ev_done) != hipSuccess) return set_err(h, ARIMA_E_DEVICE, "stats: device error");
+        finish_stats(h);
+    }
     *out = h->stats;
+    return ARIMA_OK;
+}
+
+int arima_synchronize(arima_handle *h) {
+    if (!h) return ARIMA_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    HIPCHK(h, hipSetDevice(h->device));
+    if (h->has_done) HIPCHK(h, hipEventSynchronize(h->ev_done));
     return ARIMA_OK;
 }
 
@@ -183,12 +223,23 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
     if (!h || !name) return ARIMA_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
     if (!strcmp(name, "smear")) { h->smear = value ? 1 : 0; return ARIMA_OK; }
-    if (!strcmp(name, "g_permille")) { h->g_permille = (int)std::min<int64_t>(1000, std::max<int64_t>(0, value)); return ARIMA_OK; }
     if (!strcmp(name, "grid_blocks")) { h->grid_blocks_override = (int)std::max<int64_t>(0, value); return ARIMA_OK; }
     return set_err(h, ARIMA_E_INVALID_ARG, "unknown option");
 }
 
 // ---------------------------------------------------------------------------------------------------------
+// Every device call waits (on the device, not the host) for the previous call's work: the handle's workspaces are
+// shared by all calls, whichever stream they are issued on.
+static void begin_call(arima_handle *h, hipStream_t s) {
+    if (h->has_done) hipStreamWaitEvent(s, h->ev_done, 0);
+}
+
+static hipError_t end_call(arima_handle *h, hipStream_t s) {
+    hipError_t e = hipEventRecord(h->ev_done, s);
+    if (e == hipSuccess) h->has_done = true;
+    return e;
+}
+
 static int fit_device_locked(arima_handle *h, const double *d_series, int64_t N, int32_t T, int64_t ld, int32_t p,
                              int32_t d, int32_t q, int32_t I, int32_t method, const double *d_user_init,
                              double *d_coef, double *d_ll, int32_t *d_status, int32_t *d_neval, int32_t *d_ngrad,
@@ -200,14 +251,15 @@ static int fit_device_locked(arima_handle *h, const double *d_series, int64_t N,
     const int k = I + p + q;
     const int n = std::max(T - d, 0);
     const int64_t ldn = round_up(std::max(n, 1), 16);
-    arima_fit_stats st{};
-    st.n_series = N;
-    h->stats = st;
+    h->pending = PendingStats{};
+    h->stats = arima_fit_stats{};
     if (N == 0) return ARIMA_OK;
+    begin_call(h, s);
 
     RCCHK(h, h->diff.ensure((size_t)N * ldn * sizeof(double)), "workspace");
-    RCCHK(h, h->ctl.ensure(16 * sizeof(unsigned long long)), "workspace");
-    HIPCHK(h, hipMemsetAsync(h->ctl.ptr, 0, 16 * sizeof(unsigned long long), s));
+    RCCHK(h, h->ctl.ensure(kCtlWords * sizeof(unsigned long long)), "workspace");
+    HIPCHK(h, hipMemsetAsync(h->ctl.ptr, 0, kCtlWords * sizeof(unsigned long long), s));
+    HIPCHK(h, hipMemsetAsync(h->ctl.as<unsigned long long>() + 15, 0xff, sizeof(unsigned long long), s));
 
     HIPCHK(h, hipEventRecord(h->ev[0], s));
     RCCHK(h, sts::launch_difference(d_series, ld, h->diff.as<double>(), ldn, N, T, d, 1, s), "difference");
@@ -238,23 +290,42 @@ static int fit_device_locked(arima_handle *h, const double *d_series, int64_t N,
                                d_status, d_neval, d_ngrad, d_flags);
             HIPCHK(h, hipGetLastError());
         } else {
+            // one persistent workgroup per CU (4 waves x the kernel's optimizer slots); fewer when the batch
+            // cannot fill them
             int blocks = h->grid_blocks_override;
-            if (blocks <= 0) {
-                const int per_cu = std::max(1, sts::cg_fit_occupancy_blocks(p, q, I, h->smear));
-                blocks = per_cu * std::max(1, h->num_cus);
-            }
-            const int64_t need = (N + 255) / 256;
+            if (blocks <= 0) blocks = std::max(1, h->num_cus);
+            const int per_block = std::max(1, sts::cg_fit_series_per_block(p, q, I));
+            const int64_t need = (N + per_block - 1) / per_block;
             if (blocks > need) blocks = (int)need;
             h->last_grid = blocks;
             RCCHK(h, sts::launch_cg_fit(y, ldn, n, N, p, q, I, h->smear, init, init_status, d_coef, d_ll, d_status,
-                                        d_neval, d_ngrad, d_flags, h->ctl.as<unsigned long long>(), blocks,
-                                        h->g_permille, s),
+                                        d_neval, d_ngrad, d_flags, h->ctl.as<unsigned long long>(), blocks, s),
                   "cg_fit");
         }
         HIPCHK(h, hipEventRecord(h->ev[3], s));
     }
-    HIPCHK(h, hipMemcpyAsync(h->ctl_host, h->ctl.ptr, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-    HIPCHK(h, hipStreamSynchronize(s));
+    HIPCHK(h, hipMemcpyAsync(h->ctl_host, h->ctl.ptr, kCtlWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, end_call(h, s));
+    PendingStats &ps = h->pending;
+    ps.N = N;
+    ps.n = n;
+    ps.p = p;
+    ps.q = q;
+    ps.I = I;
+    ps.ar_only = p > 0 && q == 0;
+    ps.user_init = d_user_init != nullptr;
+    ps.cg = !ps.ar_only && method == ARIMA_METHOD_CSS_CGD && k > 0;
+    ps.grid = h->last_grid;
+    ps.valid = true;
+    return ARIMA_OK;
+}
+
+// Completes the stats of the last fit once its device work has finished (arima_get_last_stats).
+static void finish_stats(arima_handle *h) {
+    const PendingStats &ps = h->pending;
+    arima_fit_stats st{};
+    const int64_t N = ps.N;
+    const int n = ps.n, p = ps.p, q = ps.q, I = ps.I, k = I + p + q;
     float ms = 0;
     hipEventElapsedTime(&ms, h->ev[0], h->ev[1]);
     st.ms_difference = ms;
@@ -273,21 +344,28 @@ static int fit_device_locked(arima_handle *h, const double *d_series, int64_t N,
     st.wave_g_passes = (int64_t)c[4];
     st.spec_hits = (int64_t)c[7];
     st.wave_multi_passes = (int64_t)c[8];
-    st.grid_blocks = h->last_grid;
-    for (int i = 0; i < 6; ++i) st.diag[i] = (int64_t)c[10 + i];
+    st.spec_chains = (int64_t)c[9];
+    // STS_TIMING builds: F-pass, G-pass, advance, select cycles (summed over waves), kernel span, drained time
+    st.diag[0] = (int64_t)c[10];
+    st.diag[1] = (int64_t)c[11];
+    st.diag[2] = (int64_t)c[12];
+    st.diag[3] = (int64_t)c[13];
+    st.diag[4] = c[14] ? (int64_t)(c[14] - c[15]) : 0;
+    st.diag[5] = (int64_t)c[16];
+    st.grid_blocks = ps.grid;
     // HR passes: 2 per column of each of the two least squares (+1 re-transform sweep over C rows)
     const int M = std::max(p, q), m = M + 1;
-    if (p > 0 && q == 0) st.hr_passes = N * (int64_t)(2 * (I + p));
-    else if (!d_user_init) st.hr_passes = N * (int64_t)(2 * (1 + m) + 2 * k);
+    if (ps.ar_only) st.hr_passes = N * (int64_t)(2 * (I + p));
+    else if (!ps.user_init) st.hr_passes = N * (int64_t)(2 * (1 + m) + 2 * k);
     // algorithmic flops: U*S*(2(p+q)+4) + G*S*(2(p+q)+4 + 2kq + 1+p+q + 2k) + W_HR
     const double S = std::max(n - M, 0);
     const double ff = 2.0 * (p + q) + 4, fg = ff + 2.0 * k * q + 1 + p + q + 2.0 * k;
     const double whr = (double)N * (3.0 * std::max(n - m, 0) * (m + 1) * (m + 1) +
                                     3.0 * std::max(n - 2 * M - 1, 0) * k * k + 2.0 * std::max(n - m, 0) * m);
-    st.flops = (double)st.f_passes * S * ff + (double)st.g_passes * S * fg + (d_user_init ? 0.0 : whr);
+    st.flops = (double)st.f_passes * S * ff + (double)st.g_passes * S * fg + (ps.user_init ? 0.0 : whr);
     st.n_series = N;
     h->stats = st;
-    return ARIMA_OK;
+    h->pending.valid = false;
 }
 
 int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_series, int32_t T, int64_t ld,
@@ -298,6 +376,7 @@ int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_se
     if (!h) return ARIMA_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    begin_call(h, s);
     return fit_device_locked(h, d_series, n_series, T, ld, p, d, q, include_intercept, method, d_user_init,
                              d_coef_out, d_css_ll_out, d_status_out, d_n_eval_out, d_n_grad_out, d_flags_out, s);
 }
@@ -315,6 +394,7 @@ int arima_fit_batch(arima_handle *h, const double *series, int64_t N, int32_t T,
     const int k = I + p + q;
     const size_t kk = (size_t)std::max(k, 1);
     hipStream_t s = h->stream;
+    begin_call(h, s);
     RCCHK(h, h->h_series.ensure((size_t)N * std::max(T, 1) * sizeof(double)), "staging");
     RCCHK(h, h->h_coef.ensure((size_t)N * kk * sizeof(double)), "staging");
     RCCHK(h, h->h_ll.ensure((size_t)N * sizeof(double)), "staging");
@@ -342,6 +422,7 @@ int arima_fit_batch(arima_handle *h, const double *series, int64_t N, int32_t T,
     if (n_eval_out) HIPCHK(h, hipMemcpyAsync(n_eval_out, h->h_neval.ptr, (size_t)N * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     if (n_grad_out) HIPCHK(h, hipMemcpyAsync(n_grad_out, h->h_ngrad.ptr, (size_t)N * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     if (flags_out) HIPCHK(h, hipMemcpyAsync(flags_out, h->h_flags.ptr, (size_t)N, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, end_call(h, s));
     HIPCHK(h, hipStreamSynchronize(s));
     return ARIMA_OK;
 }
@@ -355,12 +436,14 @@ int arima_difference_batch(arima_handle *h, const double *series, int64_t N, int
     if (N == 0 || T == 0) return ARIMA_OK;
     HIPCHK(h, hipSetDevice(h->device));
     hipStream_t s = h->stream;
+    begin_call(h, s);
     const size_t bytes = (size_t)N * T * sizeof(double);
     RCCHK(h, h->h_series.ensure(bytes), "staging");
     RCCHK(h, h->h_aux.ensure(bytes), "staging");
     HIPCHK(h, hipMemcpyAsync(h->h_series.ptr, series, bytes, hipMemcpyHostToDevice, s));
     RCCHK(h, sts::launch_difference(h->h_series.as<double>(), T, h->h_aux.as<double>(), T, N, T, d, 0, s), "difference");
     HIPCHK(h, hipMemcpyAsync(out, h->h_aux.ptr, bytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, end_call(h, s));
     HIPCHK(h, hipStreamSynchronize(s));
     return ARIMA_OK;
 }
@@ -372,6 +455,7 @@ int arima_inverse_difference_batch(arima_handle *h, const double *series, int64_
     if (N == 0 || T == 0) return ARIMA_OK;
     HIPCHK(h, hipSetDevice(h->device));
     hipStream_t s = h->stream;
+    begin_call(h, s);
     const size_t bytes = (size_t)N * T * sizeof(double);
     RCCHK(h, h->h_series.ensure(bytes), "staging");
     RCCHK(h, h->h_aux.ensure(bytes), "staging");
@@ -379,6 +463,7 @@ int arima_inverse_difference_batch(arima_handle *h, const double *series, int64_
     RCCHK(h, sts::launch_inverse_difference(h->h_series.as<double>(), T, h->h_aux.as<double>(), T, N, T, d, s),
           "inverse_difference");
     HIPCHK(h, hipMemcpyAsync(out, h->h_aux.ptr, bytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, end_call(h, s));
     HIPCHK(h, hipStreamSynchronize(s));
     return ARIMA_OK;
 }
@@ -403,6 +488,7 @@ int arima_css_loglik_batch(arima_handle *h, const double *series, int64_t N, int
     if (N == 0) return ARIMA_OK;
     HIPCHK(h, hipSetDevice(h->device));
     hipStream_t s = h->stream;
+    begin_call(h, s);
     const int k = I + p + q;
     const int n = std::max(T - d, 0);
     const int64_t ldn = round_up(std::max(n, 1), 16);
@@ -416,6 +502,7 @@ int arima_css_loglik_batch(arima_handle *h, const double *series, int64_t N, int
     RCCHK(h, sts::launch_css_loglik(h->diff.as<double>(), ldn, n, N, p, q, I, h->h_coef.as<double>(),
                                     h->h_ll.as<double>(), s), "css_loglik");
     HIPCHK(h, hipMemcpyAsync(ll_out, h->h_ll.ptr, (size_t)N * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, end_call(h, s));
     HIPCHK(h, hipStreamSynchronize(s));
     return ARIMA_OK;
 }
@@ -430,6 +517,7 @@ int arima_css_gradient_batch(arima_handle *h, const double *diffed, int64_t N, i
     if (N == 0 || k == 0) return ARIMA_OK;
     HIPCHK(h, hipSetDevice(h->device));
     hipStream_t s = h->stream;
+    begin_call(h, s);
     int64_t ld = 0;
     RCCHK(h, upload_padded(h, diffed, N, n, &ld, s), "upload");
     RCCHK(h, h->h_coef.ensure((size_t)N * k * sizeof(double)), "staging");
@@ -438,6 +526,7 @@ int arima_css_gradient_batch(arima_handle *h, const double *diffed, int64_t N, i
     RCCHK(h, sts::launch_css_grad(h->diff.as<double>(), ld, n, N, p, q, I, h->smear, h->h_coef.as<double>(),
                                   h->h_aux.as<double>(), s), "css_grad");
     HIPCHK(h, hipMemcpyAsync(grad_out, h->h_aux.ptr, (size_t)N * k * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, end_call(h, s));
     HIPCHK(h, hipStreamSynchronize(s));
     return ARIMA_OK;
 }
@@ -451,6 +540,7 @@ int arima_hannan_rissanen_batch(arima_handle *h, const double *diffed, int64_t N
     if (N == 0) return ARIMA_OK;
     HIPCHK(h, hipSetDevice(h->device));
     hipStream_t s = h->stream;
+    begin_call(h, s);
     const int k = I + p + q;
     int64_t ld = 0;
     RCCHK(h, upload_padded(h, diffed, N, n, &ld, s), "upload");
@@ -460,6 +550,7 @@ int arima_hannan_rissanen_batch(arima_handle *h, const double *diffed, int64_t N
                                  h->h_status.as<int32_t>(), s), "hr_init");
     if (k > 0) HIPCHK(h, hipMemcpyAsync(init_out, h->h_coef.ptr, (size_t)N * k * sizeof(double), hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipMemcpyAsync(status_out, h->h_status.ptr, (size_t)N * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, end_call(h, s));
     HIPCHK(h, hipStreamSynchronize(s));
     return ARIMA_OK;
 }
@@ -472,12 +563,14 @@ int arima_model_flags_batch(arima_handle *h, const double *coef, int64_t N, int3
     if (N <= 0) return ARIMA_OK;
     HIPCHK(h, hipSetDevice(h->device));
     hipStream_t s = h->stream;
+    begin_call(h, s);
     const int k = I + p + q;
     RCCHK(h, h->h_coef.ensure((size_t)N * std::max(k, 1) * sizeof(double)), "staging");
     RCCHK(h, h->h_flags.ensure((size_t)N), "staging");
     if (k > 0) HIPCHK(h, hipMemcpyAsync(h->h_coef.ptr, coef, (size_t)N * k * sizeof(double), hipMemcpyHostToDevice, s));
     RCCHK(h, sts::launch_model_flags(h->h_coef.as<double>(), N, p, q, I, h->h_flags.as<uint8_t>(), s), "flags");
     HIPCHK(h, hipMemcpyAsync(flags_out, h->h_flags.ptr, (size_t)N, hipMemcpyDeviceToHost, s));
+    HIPCHK(h, end_call(h, s));
     HIPCHK(h, hipStreamSynchronize(s));
     return ARIMA_OK;
 }
@@ -492,6 +585,7 @@ int arima_forecast_batch(arima_handle *h, const double *series, int64_t N, int32
     if (!series || !coef || !out) return set_err(h, ARIMA_E_INVALID_ARG, "null buffer");
     HIPCHK(h, hipSetDevice(h->device));
     hipStream_t s = h->stream;
+    begin_call(h, s);
     const int k = I + p + q;
     const int64_t L = (int64_t)T + n_future;
     RCCHK(h, h->h_series.ensure((size_t)N * std::max(T, 1) * sizeof(double)), "staging");
@@ -502,6 +596,7 @@ int arima_forecast_batch(arima_handle *h, const double *series, int64_t N, int32
     RCCHK(h, sts::launch_forecast(h->h_series.as<double>(), T, h->h_coef.as<double>(), k, h->h_aux.as<double>(), L, N,
                                   T, p, d, q, I, n_future, s), "forecast");
     if (L > 0) HIPCHK(h, hipMemcpyAsync(out, h->h_aux.ptr, (size_t)N * L * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, end_call(h, s));
     HIPCHK(h, hipStreamSynchronize(s));
     return ARIMA_OK;
 }
@@ -518,8 +613,10 @@ int arima_forecast_batch_device(arima_handle *h, const double *d_series, int64_t
     if (!d_series || !d_coef || !d_out) return set_err(h, ARIMA_E_INVALID_ARG, "null buffer");
     HIPCHK(h, hipSetDevice(h->device));
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    begin_call(h, s);
     RCCHK(h, sts::launch_forecast(d_series, ld, d_coef, I + p + q, d_out, ld_out, N, T, p, d, q, I, n_future, s),
           "forecast");
+    HIPCHK(h, end_call(h, s));
     return ARIMA_OK;
 }
 
@@ -572,8 +669,12 @@ int arima_order_search_batch_device(arima_handle *h, const double *d_series, int
     if (!h) return ARIMA_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
-    return order_search_locked(h, d_series, n_series, T, ld, max_p, max_d, max_q, intercept_mode, method,
-                               d_order_out, d_coef_out, d_aic_out, nullptr, s);
+    begin_call(h, s);
+    const int rc = order_search_locked(h, d_series, n_series, T, ld, max_p, max_d, max_q, intercept_mode, method,
+                                       d_order_out, d_coef_out, d_aic_out, nullptr, s);
+    if (rc != ARIMA_OK) return rc;
+    HIPCHK(h, end_call(h, s));
+    return ARIMA_OK;
 }
 
 int arima_order_search_batch(arima_handle *h, const double *series, int64_t N, int32_t T, int32_t max_p,
@@ -586,6 +687,7 @@ int arima_order_search_batch(arima_handle *h, const double *series, int64_t N, i
     if (!series || !order_out || !coef_out || !aic_out) return set_err(h, ARIMA_E_INVALID_ARG, "null buffer");
     HIPCHK(h, hipSetDevice(h->device));
     hipStream_t s = h->stream;
+    begin_call(h, s);
     RCCHK(h, h->h_series.ensure((size_t)N * std::max(T, 1) * sizeof(double)), "staging");
     RCCHK(h, h->h_aux.ensure((size_t)N * 11 * sizeof(double)), "staging");
     RCCHK(h, h->h_ll.ensure((size_t)N * sizeof(double)), "staging");
@@ -597,6 +699,7 @@ int arima_order_search_batch(arima_handle *h, const double *series, int64_t N, i
     HIPCHK(h, hipMemcpyAsync(order_out, h->os_order.ptr, (size_t)N * 4 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipMemcpyAsync(coef_out, h->h_aux.ptr, (size_t)N * 11 * sizeof(double), hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipMemcpyAsync(aic_out, h->h_ll.ptr, (size_t)N * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, end_call(h, s));
     HIPCHK(h, hipStreamSynchronize(s));
     return ARIMA_OK;
 }
@@ -609,12 +712,9 @@ int arima_sample_batch_device(arima_handle *h, double *d_series, int64_t N, int3
     RCCHK(h, check_orders(h, p, d, q, I), "orders");
     HIPCHK(h, hipSetDevice(h->device));
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
-    const int k = I + p + q;
-    RCCHK(h, h->h_aux.ensure((size_t)std::max(k, 1) * sizeof(double)), "staging");
-    if (k > 0) HIPCHK(h, hipMemcpyAsync(h->h_aux.ptr, base_coef, (size_t)k * sizeof(double), hipMemcpyHostToDevice, s));
-    RCCHK(h, sts::launch_sample(d_series, ld, N, T, p, d, q, I, h->h_aux.as<double>(), jitter, seed, first_series, s),
-          "sample");
-    HIPCHK(h, hipStreamSynchronize(s));
+    begin_call(h, s);
+    RCCHK(h, sts::launch_sample(d_series, ld, N, T, p, d, q, I, base_coef, jitter, seed, first_series, s), "sample");
+    HIPCHK(h, end_call(h, s));
     return ARIMA_OK;
 }
 

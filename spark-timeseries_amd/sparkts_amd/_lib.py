@@ -48,7 +48,7 @@ EXPORTED = [
     "arima_difference_batch", "arima_inverse_difference_batch", "arima_css_loglik_batch",
     "arima_css_gradient_batch", "arima_hannan_rissanen_batch", "arima_forecast_batch", "arima_model_flags_batch",
     "arima_sample_batch_device", "arima_order_search_batch", "arima_order_search_batch_device",
-    "arima_forecast_batch_device",
+    "arima_forecast_batch_device", "arima_synchronize",
 ]
 
 
@@ -58,7 +58,8 @@ class FitStats(ctypes.Structure):
                 ("flops", ctypes.c_double), ("ms_difference", ctypes.c_double), ("ms_hr_init", ctypes.c_double),
                 ("ms_cg_fit", ctypes.c_double), ("ms_total", ctypes.c_double),
                 ("wave_f_passes", ctypes.c_int64), ("wave_g_passes", ctypes.c_int64), ("grid_blocks", ctypes.c_int64),
-                ("spec_hits", ctypes.c_int64), ("wave_multi_passes", ctypes.c_int64), ("diag", ctypes.c_int64 * 6)]
+                ("spec_hits", ctypes.c_int64), ("wave_multi_passes", ctypes.c_int64), ("spec_chains", ctypes.c_int64),
+                ("diag", ctypes.c_int64 * 6)]
 
     def as_dict(self):
         d = {name: getattr(self, name) for name, _ in self._fields_}
@@ -111,6 +112,7 @@ def load():
         L.arima_num_params.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.arima_get_last_stats.argtypes = [H, ctypes.POINTER(FitStats)]
         L.arima_set_option.argtypes = [H, ctypes.c_char_p, _i64]
+        L.arima_synchronize.argtypes = [H]
         L.arima_fit_batch.argtypes = [H, _dp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _dp, _dp, _dp, _i32p,
                                       _i32p, _i32p, _u8p]
         L.arima_fit_batch_device.argtypes = [H, _vp, _i64, _i32, _i64, _i32, _i32, _i32, _i32, _i32, _vp, _vp, _vp,
@@ -171,6 +173,10 @@ class Engine:
     def set_option(self, name, value):
         self._check(self.L.arima_set_option(self.h, name.encode(), int(value)), "arima_set_option")
 
+    def synchronize(self):
+        """Wait for the device work of every call issued on this handle (the *_device calls are asynchronous)."""
+        self._check(self.L.arima_synchronize(self.h), "arima_synchronize")
+
     def stats(self):
         s = FitStats()
         self._check(self.L.arima_get_last_stats(self.h, ctypes.byref(s)), "arima_get_last_stats")
@@ -199,21 +205,28 @@ class Engine:
         self._check(rc, "arima_fit_batch")
         return dict(coef=coef[:, :k], ll=ll, status=status, n_eval=n_eval, n_grad=n_grad, flags=flags)
 
+    # The *_device methods below wrap asynchronous ABI calls. With blocking=True (the default) they wait for the
+    # call's device work before returning, so results can be read through any stream (torch's included); pass
+    # blocking=False to keep the ABI's asynchrony and call synchronize() (or stats()) later.
     def fit_batch_device(self, d_series, n_series, T, ld, p, d, q, include_intercept, d_coef, d_ll, d_status,
                          d_n_eval=None, d_n_grad=None, d_flags=None, d_user_init=None, method=METHOD_CSS_CGD,
-                         stream=None):
+                         stream=None, blocking=True):
         """Device-pointer entry (ints = raw HBM addresses, e.g. torch tensor .data_ptr())."""
         rc = self.L.arima_fit_batch_device(self.h, d_series, n_series, T, ld, p, d, q, int(bool(include_intercept)),
                                            method, d_user_init, d_coef, d_ll, d_status, d_n_eval, d_n_grad, d_flags,
                                            stream)
         self._check(rc, "arima_fit_batch_device")
+        if blocking:
+            self.synchronize()
 
     def sample_device(self, d_series, n_series, T, ld, p, d, q, include_intercept, base_coef, jitter, seed,
-                      first_series=0, stream=None):
+                      first_series=0, stream=None, blocking=True):
         base = np.ascontiguousarray(base_coef, dtype=np.float64)
         rc = self.L.arima_sample_batch_device(self.h, d_series, n_series, T, ld, p, d, q, int(bool(include_intercept)),
                                               _ptr(base), float(jitter), int(seed), int(first_series), stream)
         self._check(rc, "arima_sample_batch_device")
+        if blocking:
+            self.synchronize()
 
     # ---- building blocks ---------------------------------------------------------------------------------
     def difference(self, series, d):
@@ -272,18 +285,22 @@ class Engine:
         return out
 
     def forecast_device(self, d_series, n_series, T, ld, p, d, q, include_intercept, d_coef, n_future, d_out, ld_out,
-                        stream=None):
+                        stream=None, blocking=True):
         """Device-pointer forecast (ints = raw HBM addresses)."""
         self._check(self.L.arima_forecast_batch_device(self.h, d_series, n_series, T, ld, p, d, q,
                                                        int(bool(include_intercept)), d_coef, n_future, d_out, ld_out,
                                                        stream), "arima_forecast_batch_device")
+        if blocking:
+            self.synchronize()
 
     def order_search_device(self, d_series, n_series, T, ld, max_p, max_d, max_q, intercept_mode, d_order, d_coef,
-                            d_aic, method=METHOD_CSS_CGD, stream=None):
+                            d_aic, method=METHOD_CSS_CGD, stream=None, blocking=True):
         """Device-pointer order search (ints = raw HBM addresses)."""
         self._check(self.L.arima_order_search_batch_device(self.h, d_series, n_series, T, ld, max_p, max_d, max_q,
                                                            intercept_mode, method, d_order, d_coef, d_aic, stream),
                     "arima_order_search_batch_device")
+        if blocking:
+            self.synchronize()
 
     def order_search(self, series, max_p=5, max_d=2, max_q=5, intercept_mode=2, method=METHOD_CSS_CGD):
         """Min-approxAIC model over the (d, p, q, intercept) grid per series (see include/sparkts_arima.h).

@@ -267,3 +267,29 @@ def test_order_search_matches_oracle(engine, grid):
         assert np.all(order[:, 0] >= 0)      # the full C5 grid finds a qualifying model for every series
     else:
         assert np.any(order[:, 0] >= 0) or max_d == 0
+
+
+def _near_unit_root_coefs(eps_list):
+    """ARIMA(2,0,2)+c coefficient rows whose AR and MA polynomials have roots at radius 1 +- eps (real pairs and
+    complex pairs), the boundary that isStationary / isInvertible decide (ARIMA.scala:777-815)."""
+    rows = []
+    for eps in eps_list:
+        for r in (1.0 + eps, 1.0 - eps):
+            for w in (0.0, 0.7, 2.1):
+                if w == 0.0:                     # real roots r and 3: (1 - x/r)(1 - x/3)
+                    a1, a2 = 1.0 / r + 1.0 / 3.0, -1.0 / (3.0 * r)
+                else:                            # complex pair r e^{+-iw}
+                    a1, a2 = 2.0 * np.cos(w) / r, -1.0 / (r * r)
+                rows.append([0.5, a1, a2, 0.2, 0.1])       # AR side on the boundary, MA well inside
+                rows.append([0.5, 0.2, 0.1, -a1, -a2])     # MA side on the boundary (1 + th1 x + th2 x^2)
+    return np.array(rows)
+
+
+def test_model_flags_near_unit_circle(engine):
+    # ADVICE r1: the GPU uses a Schur-Cohn step-down, the reference companion-matrix eigenvalues. Both must agree
+    # for roots 1e-12 .. 1e-6 away from |z| = 1 (beyond that the answer is below the eigen-solver's own rounding
+    # and the reference itself is implementation-defined: DESIGN.md 5.2).
+    coef = _near_unit_root_coefs([1e-6, 1e-9, 1e-12])
+    f = engine.model_flags(coef, 2, 2, True)
+    exp = np.array([O.model_flags(c, 2, 2, 1) for c in coef])
+    assert np.array_equal(f, exp), np.nonzero(f != exp)

@@ -70,3 +70,36 @@ def test_gloo_world2_shards_match_single_process(tmp_path, world):
     out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     assert "MULTIRANK_OK" in out.stdout
+
+
+def _bench(*extra):
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run"] + list(extra)
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    import json
+    return json.loads(lines[0])
+
+
+def test_bench_launcher_starts_n_ranks_weak():
+    # `bench.py --gpus 2` without a torch.distributed environment starts 2 ranks itself (bench.py:launch_ranks);
+    # rank 0 reports the real world size and every rank owns its own 1M-series block (weak scaling)
+    r = _bench("--gpus", "2")
+    assert r["n_gpus"] == 2 and r["scaling"] == "weak" and r["total_series"] == 2 << 20
+    assert [tuple(s) for s in r["shards"]] == [(0, 1 << 20), (1 << 20, 2 << 20)]
+
+
+def test_bench_launcher_strong_scaling_partitions_total():
+    # configs[2]: a fixed total (8M) split into contiguous ranges, one per rank
+    r = _bench("--gpus", "2", "--total-series", str(8 << 20))
+    assert r["n_gpus"] == 2 and r["scaling"] == "strong" and r["total_series"] == 8 << 20
+    shards = [tuple(s) for s in r["shards"]]
+    assert shards[0][0] == 0 and shards[-1][1] == 8 << 20 and shards[0][1] == shards[1][0]
+
+
+def test_bench_single_rank_dry_run():
+    r = _bench()
+    assert r["n_gpus"] == 1 and [tuple(s) for s in r["shards"]] == [(0, 1 << 20)]
