@@ -209,7 +209,7 @@ __device__ __forceinline__ void css_pass(const double *__restrict__ row, int n,
 #pragma unroll
             for (int j = 0; j < K; ++j)                               // :492-499
 #pragma unroll
-                for (int kk = 0; kk < Q; ++kk) dE[0][j] = dE[0][j] - c[I + P + kk] * dE[SMEAR ? 1 : kk + 1][j];
+                for (int kk = 0; kk < Q; ++kk) dE[0][j] = dE[0][j] - c[I + P + kk] * dE[SMEAR ? DER - 1 : kk + 1][j];
             double yh = yh0;                                          // :502
             if constexpr (K > 0) dE[0][0] = dE[0][0] - (double)I;     // :503
 #pragma unroll
@@ -298,6 +298,110 @@ __device__ __forceinline__ void css_pass_multi(const double *__restrict__ row, i
     stream_elems<kPrefetchF>(row, M, n, step);
 #pragma unroll
     for (int h = 0; h < NCH; ++h) css_out[h] = css[h];
+}
+
+// ------------------------------------------------------------------------------------------------------
+// Passes over a series held in LDS by a whole wave (the express path of k_cg_fit: one long-running series per
+// wave). Every lane reads the same element at the same step (LDS broadcast).
+//   css_row_lds       one objective chain per lane (the lanes evaluate the request's point and its predictions)
+//   grad_column_lds   gradientlogLikelihoodCSSARMA split by column: lane `col` carries column `col` of dEdTheta;
+//                     every lane also carries the shared residual recursion, so css and sigma2 come out the same
+//                     in every lane. Same operations in the same order as css_pass<..., true, SMEAR>.
+// ------------------------------------------------------------------------------------------------------
+template <int P, int Q, int I>
+__device__ __forceinline__ double css_row_lds(const double *row, int n,
+                                              const double (&c)[I + P + Q > 0 ? I + P + Q : 1]) {
+    constexpr int M = (P > Q ? P : Q);
+    constexpr int PA = P > 0 ? P : 1;
+    double yl[PA];
+#pragma unroll
+    for (int j = 0; j < PA; ++j) yl[j] = (j < P && M - 1 - j >= 0 && M - 1 - j < n) ? row[M - 1 - j] : 0.0;
+    double e1 = 0.0, e2 = 0.0, css = 0.0;
+    const double yh0 = 0.0 + (double)I * c[0];
+#pragma unroll 8
+    for (int t = M; t < n; ++t) {
+        const double yi = row[t];
+        double yh = yh0;
+#pragma unroll
+        for (int j = 0; j < P; ++j) yh = yh + yl[j] * c[I + j];
+#pragma unroll
+        for (int j = 0; j < Q; ++j) yh = yh + (j == 0 ? e1 : e2) * c[I + P + j];
+        const double e = yi - yh;
+        css = css + e * e;
+        e2 = e1;
+        e1 = e;
+        if constexpr (P > 0) {
+#pragma unroll
+            for (int j = PA - 1; j >= 1; --j) yl[j] = yl[j - 1];
+            yl[0] = yi;
+        }
+    }
+    return css;
+}
+
+template <int P, int Q, int I, bool SMEAR>
+__device__ __forceinline__ void grad_column_lds(const double *row, int n,
+                                                const double (&c)[I + P + Q > 0 ? I + P + Q : 1], int col,
+                                                double &css_out, double &g_out) {
+    constexpr int M = (P > Q ? P : Q);
+    constexpr int PA = P > 0 ? P : 1;
+    constexpr int DR = SMEAR ? 1 : (Q > 0 ? Q : 1);     // lag rows 1.. of this column
+    double yl[PA];
+#pragma unroll
+    for (int j = 0; j < PA; ++j) yl[j] = (j < P && M - 1 - j >= 0 && M - 1 - j < n) ? row[M - 1 - j] : 0.0;
+    double e1 = 0.0, e2 = 0.0, css = 0.0, sigma2 = 0.0, g = 0.0;
+    double dl[DR];                                      // dl[r] = dEdTheta(r + 1, col)
+#pragma unroll
+    for (int r = 0; r < DR; ++r) dl[r] = 0.0;
+    const double yh0 = 0.0 + (double)I * c[0];
+    const double nd = (double)n;
+#pragma unroll 4
+    for (int t = M; t < n; ++t) {
+        const double yi = row[t];
+        double d0 = 0.0;                                                // dEdTheta(0, col), reset at :528
+#pragma unroll
+        for (int kk = 0; kk < Q; ++kk) d0 = d0 - c[I + P + kk] * dl[SMEAR ? 0 : kk];   // :492-499
+        // the column's own direct term (:503, :506-510, :514-518). Column 0 also gets `- I` in the reference, which
+        // for I = 0 subtracts 0.0 (an identity) before its AR term, so one subtraction per column is exact.
+        double dv = 0.0;
+        if constexpr (I) dv = (col == 0) ? 1.0 : dv;
+        double yh = yh0;
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            yh = yh + yl[j] * c[I + j];
+            dv = (col == I + j) ? yl[j] : dv;
+        }
+#pragma unroll
+        for (int j = 0; j < Q; ++j) {
+            const double mj = (j == 0 ? e1 : e2);
+            yh = yh + mj * c[I + P + j];
+            dv = (col == I + P + j) ? mj : dv;
+        }
+        d0 = d0 - dv;
+        const double e = yi - yh;                                       // :520
+        const double e_sq = e * e;
+        sigma2 = sigma2 + e_sq / nd;                                    // :521
+        css = css + e_sq;
+        e2 = e1;                                                        // :522
+        e1 = e;
+        g = g + d0 * e;                                                 // :524
+        if constexpr (Q > 0) {                                          // :526
+            if constexpr (SMEAR) {
+                dl[0] = d0;
+            } else {
+#pragma unroll
+                for (int r = DR - 1; r >= 1; --r) dl[r] = dl[r - 1];
+                dl[0] = d0;
+            }
+        }
+        if constexpr (P > 0) {
+#pragma unroll
+            for (int j = PA - 1; j >= 1; --j) yl[j] = yl[j - 1];
+            yl[0] = yi;
+        }
+    }
+    css_out = css;
+    g_out = g / -sigma2;                                                // :532
 }
 
 // ------------------------------------------------------------------------------------------------------

@@ -341,7 +341,7 @@ __global__ __launch_bounds__(256) void k_sample(double *__restrict__ out, int64_
         }
     }
     // addTimeDependentEffects(noise): changes = [c]*M ++ noise; iterateARMA(changes, changes, +, errors = copy)
-    const double ia = I ? c[0] : 0.0;
+    const double ia = (I && K > 0) ? c[0] : 0.0;
     double hist[kSampleMaxOrder];   // hist[j] = changes(i - 1 - j)
     double ma[kSampleMaxOrder];
     for (int j = 0; j < kSampleMaxOrder; ++j) { hist[j] = ia; ma[j] = 0.0; }
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(256) void k_sample(double *__restrict__ out, int64_
             z = z1;
         }
         double v = z;                                     // dest(i) starts as the noise value
-        v = v + (double)I * c[0];
+        v = v + (double)I * (K > 0 ? c[0] : 0.0);     // `intercept * coefficients(0)` (K = 0: pure noise)
         for (int j = 0; j < p; ++j) v = v + hist[j] * c[I + j];
         for (int j = 0; j < q; ++j) v = v + ma[j] * c[I + p + j];
         for (int j = 0; j < q - 1; ++j) ma[j + 1] = ma[j];     // updateMAErrors (ascending copy)
@@ -466,11 +466,12 @@ int launch_ar_fit(const double *y, int64_t ld, int n, int64_t N, int p, int I, d
 int launch_cg_fit(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, int smear,
                   const double *init, const int32_t *init_status, double *coef_out, double *ll_out,
                   int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
-                  unsigned long long *ctl, int grid_blocks, hipStream_t s) {
+                  unsigned long long *ctl, int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready,
+                  hipStream_t s) {
     if (N == 0) return ARIMA_OK;
 #define C_(PP)                                                                                             \
     launch_cg_fit_P<PP>(y, ld, n, N, q, I, smear, init, init_status, coef_out, ll_out, status_out, n_eval_out, \
-                        n_grad_out, flags_out, ctl, grid_blocks, s)
+                        n_grad_out, flags_out, ctl, grid_blocks, express_blocks, xq, xready, s)
     STS_P_SWITCH(C_)
 #undef C_
 }

@@ -152,7 +152,7 @@ template <int K>
 __device__ __forceinline__ void write_fit(int64_t sid, int status, const double (&coef)[K], double ll, int n_eval,
                                           int n_grad, uint8_t flags, double *coef_out, double *ll_out,
                                           int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out,
-                                          uint8_t *flags_out) {
+                                          uint8_t *flags_out, int path = 1) {
     const bool ok = status == ARIMA_ST_OK;
 #pragma unroll
     for (int j = 0; j < K; ++j) coef_out[sid * K + j] = ok ? coef[j] : __builtin_nan("");
@@ -161,6 +161,11 @@ __device__ __forceinline__ void write_fit(int64_t sid, int status, const double 
     if (n_eval_out) n_eval_out[sid] = n_eval;
     if (n_grad_out) n_grad_out[sid] = n_grad;
     if (flags_out) flags_out[sid] = ok ? flags : 0;
+#ifdef STS_TIMING
+    // diagnostics build only: the finish time (100 MHz real-time counter) replaces the LL, flags = path taken
+    ll_out[sid] = (double)__builtin_amdgcn_s_memrealtime();
+    if (flags_out) flags_out[sid] = (uint8_t)path;
+#endif
 }
 
 // speculation policy per parameter count (tests/sim/cglane_sim.cpp measures it: 2 predictions per request and a
@@ -196,15 +201,202 @@ constexpr int fit_slots_per_wave() {
     return (cap / 8) * 8;
 }
 
+// ---- express path: one long-running series per wave, its row in LDS -------------------------------------
+// The launch's critical path is its slowest series (a few hundred of 1M series need 10-60x the median number of
+// passes). In the lane-per-series waves a pass costs the whole wave's instruction stream (~30-60 instructions per
+// time step), so such a series advances by one pass per wave pass. Express workgroups (the last blocks of the
+// grid) instead give a long-running series a whole wave: the row is staged once into LDS, objective passes run
+// the request's point and its predicted points on separate lanes, and gradient passes split dEdTheta's columns
+// over lanes — a pass then costs about one chain of instructions. Hand-off: an idle express wave takes a ticket
+// (ctl[20]); a bulk wave that sees an unserved ticket donates its oldest slot with >= kDonateEvals evaluations
+// into the ring entry of the next fill index (ctl[21]) and publishes it (release, then the entry's ready word =
+// index + 1); the express wave polls its entry's ready word (acquire). Express waves exit once every bulk wave has
+// finished (ctl[22]) and no fill is left for their ticket, so they never hold up the launch.
+constexpr int kExpressRing = 2048;           // ring entries (>= express waves + bulk waves: no entry is overwritten live)
+constexpr int kExpressEntryBytes = 512;      // ring stride reserved per entry (>= sizeof(FitSlotCore<K>) for K <= 11)
+#ifndef STS_EXPRESS_GROUPS
+#define STS_EXPRESS_GROUPS 2
+#endif
+constexpr int kExpressGroups = STS_EXPRESS_GROUPS;   // series per express wave (at most; LDS permitting)
+constexpr int kDonateEvals = 256;            // a slot is donated only after this many evaluations ...
+constexpr int kDonateEvalsDrained = 32;      // ... or this many once the batch's work counter has run out
+
+template <int K>
+constexpr int express_state_bytes() { return (int)((sizeof(FitSlotCore<K>) + 15) / 16 * 16); }
+
+// longest differenced series an express wave can stage next to its state and exchange area (per-wave LDS share)
+template <int K>
+constexpr int express_max_n(int lds_per_wave) { return (lds_per_wave - express_state_bytes<K>() - 16 * 8) / 8 - 1; }
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int K>
+__device__ __forceinline__ void copy_core(FitSlotCore<K> *dst, const FitSlotCore<K> *src, int lane) {
+    static_assert(sizeof(FitSlotCore<K>) % 8 == 0, "8-byte words");
+    constexpr int W = (int)(sizeof(FitSlotCore<K>) / 8);
+    const unsigned long long *s = reinterpret_cast<const unsigned long long *>(src);
+    unsigned long long *d = reinterpret_cast<unsigned long long *>(dst);
+    for (int w = lane; w < W; w += 64) d[w] = s[w];
+}
+
+// Express wave: up to XG long series at once, one per group of 64/XG lanes (XG from the row length: each group
+// needs its state, its row and an exchange area in the wave's LDS share). Each group holds either a series or an
+// outstanding ticket. Per iteration: groups poll their ticket's ring entry (non-blocking) and load what arrived;
+// then one objective pass serves every group that wants F (lane l of a group evaluates chain l: the request's
+// point, then its predicted points) and one gradient pass every group that wants G (lane l carries dEdTheta's
+// column l); lane 0 of each group advances its state machine. A group whose ticket can no longer be filled
+// (every bulk wave done and the fills below the ticket) retires; the wave exits when all its groups retired.
+template <int K>
+constexpr int express_group_bytes(int n) { return express_state_bytes<K>() + ((n + 1) & ~1) * 8 + 16 * 8; }
+
+template <int P, int Q, int I, bool SMEAR>
+__device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__restrict__ y, int64_t ld, int n,
+                            double *__restrict__ coef_out, double *__restrict__ ll_out,
+                            int32_t *__restrict__ status_out, int32_t *__restrict__ n_eval_out,
+                            int32_t *__restrict__ n_grad_out, uint8_t *__restrict__ flags_out,
+                            unsigned long long *__restrict__ ctl, unsigned char *__restrict__ xq,
+                            unsigned *__restrict__ xready, unsigned long long bulk_waves, int lane) {
+    constexpr int K = I + P + Q;
+    constexpr int NS = spec_ns<K>();
+    const int gbytes = express_group_bytes<K>(n);
+    int XG = lds_bytes / gbytes;
+    XG = XG >= kExpressGroups ? kExpressGroups : (XG >= 2 ? 2 : 1);
+    const int GL = 64 / XG;                                 // lanes per group
+    const int grp = lane / GL, gl = lane % GL;
+    const bool glead = gl == 0;
+    unsigned char *gbase = lds + grp * gbytes;
+    FitSlotCore<K> &ES = *reinterpret_cast<FitSlotCore<K> *>(gbase);
+    double *row = reinterpret_cast<double *>(gbase + express_state_bytes<K>());
+    double *xch = row + ((n + 1) & ~1);                     // K + NS + 1 doubles
+    unsigned long long served = 0, pf = 0, pg = 0, evals = 0, grads = 0, hits = 0;
+    // group state: 0 = waiting on ticket, 1 = fitting, 2 = retired (wave-uniform per group after each shfl)
+    int gstate = 0;
+    unsigned long long ticket = 0;
+    if (glead) ticket = atomicAdd(&ctl[20], 1ull);
+    ticket = __shfl(ticket, grp * GL);
+    for (;;) {
+        // ---- groups waiting on a ticket: poll (group leader), then load the entry (whole group) ----
+        int arrived = 0;
+        if (gstate == 0 && glead) {
+            const unsigned e = (unsigned)(ticket % kExpressRing);
+            unsigned r = __hip_atomic_load(&xready[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (r == (unsigned)(ticket + 1)) {
+                arrived = 1;
+            } else {
+                const unsigned long long bd = __hip_atomic_load(&ctl[22], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (bd >= bulk_waves) {                     // every fill has happened
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    const unsigned long long fl =
+                        __hip_atomic_load(&ctl[21], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    r = __hip_atomic_load(&xready[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    arrived = (r == (unsigned)(ticket + 1)) ? 1 : (ticket >= fl ? 2 : 0);
+                }
+            }
+            if (arrived == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
+        arrived = __shfl(arrived, grp * GL);
+        if (arrived == 2) gstate = 2;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (arrived == 1) {
+            const unsigned e = (unsigned)(ticket % kExpressRing);
+            const FitSlotCore<K> *src = reinterpret_cast<const FitSlotCore<K> *>(xq + (size_t)e * kExpressEntryBytes);
+            constexpr int W = (int)(sizeof(FitSlotCore<K>) / 8);
+            for (int w = gl; w < W; w += GL)
+                reinterpret_cast<unsigned long long *>(&ES)[w] = reinterpret_cast<const unsigned long long *>(src)[w];
+        }
+        wave_sync_lds();
+        if (arrived == 1) {
+            const double *srow = y + ES.sid * ld;
+            for (int i = gl; i < n; i += GL) row[i] = srow[i];
+            gstate = 1;
+            served += glead;
+        }
+        wave_sync_lds();
+        if (__all(gstate == 2)) break;
+        if (!__any(gstate == 1)) {                          // nothing to compute: back off
+            __builtin_amdgcn_s_sleep(16);
+            continue;
+        }
+        // ---- one pass for every group: the objective pass when all groups want F; otherwise the gradient pass,
+        //      whose lanes in F groups evaluate their chain points (the pass also yields the objective) ----
+        const int req = gstate == 1 ? (int)ES.s.req : REQ_NONE;
+        const int nsp = req == REQ_F ? (int)ES.s.rq_nspec : 0;
+        double c[K];
+        if (req == REQ_F && gl >= 1 && gl <= nsp) ES.s.spec_point(gl - 1, c);
+        else if (req != REQ_NONE) ES.s.request_point(c);
+        else {
+#pragma unroll
+            for (int j = 0; j < K; ++j) c[j] = 0.0;
+        }
+        const double *prow = gstate == 1 ? row : reinterpret_cast<double *>(lds + express_state_bytes<K>());
+        double cssv, gj = 0.0;
+        if (__any(req == REQ_G)) grad_column_lds<P, Q, I, SMEAR>(prow, n, c, gl < K ? gl : 0, cssv, gj);
+        else cssv = css_row_lds<P, Q, I>(prow, n, c);
+        if (req == REQ_F && gl <= nsp) xch[gl] = css_to_loglik(cssv, n);
+        if (req == REQ_G && gl < K) xch[gl] = gj;
+        if (req == REQ_G && glead) xch[K] = css_to_loglik(cssv, n);
+        wave_sync_lds();
+        if (glead && req == REQ_F) {
+            for (int h = 1; h <= nsp && h <= NS; ++h) ES.s.spec_store(h - 1, xch[h]);
+            double g0[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) g0[j] = 0.0;
+            ES.s.req = REQ_NONE;
+            ES.s.advance(xch[0], g0);
+            pf++;
+        } else if (glead && req == REQ_G) {
+            double g[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) g[j] = xch[j];
+            ES.s.req = REQ_NONE;
+            ES.s.advance(xch[K], g);
+            pg++;
+        }
+        wave_sync_lds();
+        // ---- finished series: write the result, take a new ticket ----
+        const bool fin = gstate == 1 && ES.s.done();
+        if (fin && glead) {
+            double pt[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) pt[j] = ES.s.point[j];
+            write_fit<K>(ES.sid, ES.s.status, pt, ES.s.prev_obj, ES.s.n_eval, ES.s.n_grad,
+                         ES.s.status == ARIMA_ST_OK ? model_flags<P, Q, I>(pt) : (uint8_t)0, coef_out, ll_out,
+                         status_out, n_eval_out, n_grad_out, flags_out, 2);
+            evals += ES.s.n_eval;
+            grads += ES.s.n_grad;
+            hits += ES.s.spec_hits;
+            ticket = atomicAdd(&ctl[20], 1ull);
+        }
+        if (fin) gstate = 0;
+        ticket = __shfl(ticket, grp * GL);
+        wave_sync_lds();
+    }
+    if (glead) {
+        atomicAdd(&ctl[5], evals);
+        atomicAdd(&ctl[6], grads);
+        atomicAdd(&ctl[7], hits);
+        atomicAdd(&ctl[23], served);
+        atomicAdd(&ctl[24], pf);
+        atomicAdd(&ctl[25], pg);
+    }
+}
+
 template <int P, int Q, int I, bool SMEAR, int SPW>
 __global__ __launch_bounds__(64 * kFitWaves, 1) void k_cg_fit(
     const double *__restrict__ y, int64_t ld, int n, int64_t N, const double *__restrict__ init,
     const int32_t *__restrict__ init_status, double *__restrict__ coef_out, double *__restrict__ ll_out,
     int32_t *__restrict__ status_out, int32_t *__restrict__ n_eval_out, int32_t *__restrict__ n_grad_out,
-    uint8_t *__restrict__ flags_out, unsigned long long *__restrict__ ctl) {
+    uint8_t *__restrict__ flags_out, unsigned long long *__restrict__ ctl, unsigned char *__restrict__ xq,
+    unsigned *__restrict__ xready, int n_bulk) {
     // ctl[0] = work counter, ctl[1] = lane F passes, ctl[2] = lane G passes, ctl[3] = wave F passes (one chain),
     // ctl[4] = wave G passes, ctl[5] = objective evaluations, ctl[6] = gradient evaluations, ctl[7] = spec hits,
-    // ctl[8] = wave F passes with speculative chains, ctl[9] = speculative chains evaluated
+    // ctl[8] = wave F passes with speculative chains, ctl[9] = speculative chains evaluated,
+    // ctl[20] = express tickets, ctl[21] = express fills (donations), ctl[22] = bulk waves finished,
+    // ctl[23] = series finished on the express path, ctl[24] / ctl[25] = express F / G passes
     constexpr int K = I + P + Q;
     constexpr int NS = spec_ns<K>();
     constexpr int NJ = (SPW + 63) / 64;      // slot groups: lane l owns slots l, l + 64, ...
@@ -212,10 +404,18 @@ __global__ __launch_bounds__(64 * kFitWaves, 1) void k_cg_fit(
     __shared__ FitSlot<K> slots[kFitWaves][SPW];
     __shared__ int assign[kFitWaves][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const bool has_express = n_bulk < (int)gridDim.x;
+    if ((int)blockIdx.x >= n_bulk) {                      // express workgroup: this wave's share of the LDS
+        fit_express<P, Q, I, SMEAR>(reinterpret_cast<unsigned char *>(&slots[wave][0]), (int)sizeof(slots[0]), y, ld,
+                                    n, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out, ctl, xq,
+                                    xready, (unsigned long long)n_bulk * kFitWaves, lane);
+        return;
+    }
     FitSlot<K> *ws = slots[wave];
     unsigned long long lane_f = 0, lane_g = 0, wave_f = 0, wave_g = 0, wave_m = 0, evals = 0, grads = 0, hits = 0,
                        chains = 0;
     unsigned round_no = 0;
+    bool drained = false;                  // the batch's work counter has run out (this wave saw it)
     const bool lane0 = lane == 0;
 #ifdef STS_TIMING
     // diagnostics build only: shader-clock cycles per phase, summed over waves (ctl[10..13]), the kernel span
@@ -241,6 +441,7 @@ __global__ __launch_bounds__(64 * kFitWaves, 1) void k_cg_fit(
                 const int64_t sid = (int64_t)(base + (unsigned long long)rank);
                 FitSlotCore<K> &S = ws[slot].c;
                 if (sid >= N) {
+                    drained = true;
 #ifdef STS_TIMING
                     if (tm_drain == 0) tm_drain = __builtin_amdgcn_s_memtime();
 #endif
@@ -421,9 +622,70 @@ __global__ __launch_bounds__(64 * kFitWaves, 1) void k_cg_fit(
             }
         }
         refill(my, need);
+        if (has_express) {
+            // an express wave is waiting: hand it this wave's oldest slot (the likely critical path)
+            unsigned long long wants = 0, filled = 0;
+            if (lane0) {
+                wants = __hip_atomic_load(&ctl[20], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                filled = __hip_atomic_load(&ctl[21], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            wants = __shfl(wants, 0);
+            filled = __shfl(filled, 0);
+            if (wants > filled) {
+                const int donate_min = __any(drained) ? kDonateEvalsDrained : kDonateEvals;
+                unsigned long long key = 0;
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    const int slot = lane + 64 * j;
+                    if (slot < SPW && ws[slot].c.sid >= 0 && ws[slot].c.s.req != REQ_NONE &&
+                        ws[slot].c.s.n_eval >= donate_min) {
+                        const unsigned long long kk = ((unsigned long long)ws[slot].c.s.n_eval << 16) | (unsigned)(slot + 1);
+                        key = kk > key ? kk : key;
+                    }
+                }
+#pragma unroll
+                for (int off = 32; off >= 1; off >>= 1) {
+                    const unsigned long long o = __shfl_xor(key, off);
+                    key = o > key ? o : key;
+                }
+                if (key) {
+                    const int bs = (int)(key & 0xffffull) - 1;
+                    unsigned long long jx = 0;
+                    if (lane0) jx = atomicAdd(&ctl[21], 1ull);
+                    jx = __shfl(jx, 0);
+                    const unsigned e = (unsigned)(jx % kExpressRing);
+                    copy_core<K>(reinterpret_cast<FitSlotCore<K> *>(xq + (size_t)e * kExpressEntryBytes), &ws[bs].c, lane);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (lane0) {
+                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        __hip_atomic_store(&xready[e], (unsigned)(jx + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    if (lane == (bs & 63)) {
+                        ws[bs].c.sid = -1;
+                        ws[bs].c.s.req = REQ_NONE;
+                    }
+                    wave_sync_lds();
+                    refill(bs, lane == (bs & 63));
+                }
+            }
+        }
 #ifdef STS_TIMING
         tm_adv += now() - t_c;
 #endif
+    }
+    if (has_express) {
+        if (lane0) {                                        // this bulk wave will fill no more express entries
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            atomicAdd(&ctl[22], 1ull);
+        }
+        // its slots are all finished: the wave serves the remaining long series on the express path, in the LDS
+        // share its slots used
+        wave_sync_lds();
+        fit_express<P, Q, I, SMEAR>(reinterpret_cast<unsigned char *>(&slots[wave][0]), (int)sizeof(slots[0]), y, ld,
+                                    n, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out, ctl, xq,
+                                    xready, (unsigned long long)n_bulk * kFitWaves, lane);
     }
 #ifdef STS_TIMING
     if (lane0) {
@@ -577,7 +839,7 @@ template <int P>
 int launch_cg_fit_P(const double *y, int64_t ld, int n, int64_t N, int q, int I, int smear, const double *init,
                     const int32_t *init_status, double *coef_out, double *ll_out, int32_t *status_out,
                     int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out, unsigned long long *ctl,
-                    int grid_blocks, hipStream_t s) {
+                    int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready, hipStream_t s) {
     return with_order(q, [&](auto Qc) {
         return with_bool(I, [&](auto Ic) {
             return with_smear(smear, [&](auto Sc) {
@@ -587,9 +849,12 @@ int launch_cg_fit_P(const double *y, int64_t ld, int n, int64_t N, int q, int I,
                     return ARIMA_E_INVALID_ARG;
                 } else {
                     constexpr int SPW = fit_slots_per_wave<P + Q + II>();
-                    hipLaunchKernelGGL((k_cg_fit<P, Q, II, S, SPW>), dim3(grid_blocks), dim3(64 * kFitWaves), 0, s,
-                                       y, ld, n, N, init, init_status, coef_out, ll_out, status_out, n_eval_out,
-                                       n_grad_out, flags_out, ctl);
+                    // express blocks only when the row fits next to the state in one wave's LDS share
+                    const int lds_per_wave = SPW * (int)sizeof(FitSlot<P + Q + II>);
+                    if (n > express_max_n<P + Q + II>(lds_per_wave)) express_blocks = 0;
+                    hipLaunchKernelGGL((k_cg_fit<P, Q, II, S, SPW>), dim3(grid_blocks + express_blocks),
+                                       dim3(64 * kFitWaves), 0, s, y, ld, n, N, init, init_status, coef_out, ll_out,
+                                       status_out, n_eval_out, n_grad_out, flags_out, ctl, xq, xready, grid_blocks);
                     STS_CHECK_LAUNCH();
                     return ARIMA_OK;
                 }
@@ -660,7 +925,8 @@ int launch_model_flags_P(const double *coef, int64_t N, int q, int I, uint8_t *f
                                          int32_t *, int32_t *, int32_t *, uint8_t *, hipStream_t);              \
     EXT template int launch_cg_fit_P<PP>(const double *, int64_t, int, int64_t, int, int, int, const double *,   \
                                          const int32_t *, double *, double *, int32_t *, int32_t *, int32_t *,  \
-                                         uint8_t *, unsigned long long *, int, hipStream_t);                     \
+                                         uint8_t *, unsigned long long *, int, int, unsigned char *, unsigned *, \
+                                         hipStream_t);                                                          \
     EXT template int cg_fit_series_per_block_P<PP>(int, int);                                                   \
     EXT template int launch_css_loglik_P<PP>(const double *, int64_t, int, int64_t, int, int, const double *,    \
                                              double *, hipStream_t);                                            \

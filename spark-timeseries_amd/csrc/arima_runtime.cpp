@@ -56,7 +56,7 @@ struct PendingStats {
     int64_t N = 0;
     int n = 0, p = 0, q = 0, I = 0;
     bool ar_only = false, user_init = false, cg = false;
-    int64_t grid = 0;
+    int64_t grid = 0, express = 0;
 };
 
 }  // namespace
@@ -74,9 +74,11 @@ struct arima_handle {
     PendingStats pending;
     int smear = 1;            // Breeze 0.12 overlap semantics at ARIMA.scala:526: element-wise copy
     int grid_blocks_override = 0;
+    int express_blocks = -1;       // k_cg_fit express workgroups (-1: num_cus / 16)
+    int64_t last_express = 0;
     int64_t last_grid = 0;
     // device workspaces
-    DevBuf diff, init, hr_status, ctl;
+    DevBuf diff, init, hr_status, ctl, xring, xready;
     // host-API staging
     DevBuf h_series, h_coef, h_ll, h_status, h_neval, h_ngrad, h_flags, h_uinit, h_aux;
     // order-search candidate buffers (one fit of the grid at a time) + host-API staging of its outputs
@@ -223,6 +225,7 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
     if (!h || !name) return ARIMA_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
     if (!strcmp(name, "smear")) { h->smear = value ? 1 : 0; return ARIMA_OK; }
+    if (!strcmp(name, "express_blocks")) { h->express_blocks = (int)std::max<int64_t>(-1, value); return ARIMA_OK; }
     if (!strcmp(name, "grid_blocks")) { h->grid_blocks_override = (int)std::max<int64_t>(0, value); return ARIMA_OK; }
     return set_err(h, ARIMA_E_INVALID_ARG, "unknown option");
 }
@@ -290,16 +293,27 @@ static int fit_device_locked(arima_handle *h, const double *d_series, int64_t N,
                                d_status, d_neval, d_ngrad, d_flags);
             HIPCHK(h, hipGetLastError());
         } else {
-            // one persistent workgroup per CU (4 waves x the kernel's optimizer slots); fewer when the batch
-            // cannot fill them
+            // one persistent workgroup per CU (4 waves x the kernel's optimizer slots), the last num_cus/16 of
+            // them express workgroups (k_cg_fit's long-series path); fewer bulk blocks when the batch cannot
+            // fill them
+            const int cus = std::max(1, h->num_cus);
+            int xblocks = h->express_blocks >= 0 ? h->express_blocks : std::max(1, cus / 16);
+            if (xblocks >= cus) xblocks = cus - 1;
             int blocks = h->grid_blocks_override;
-            if (blocks <= 0) blocks = std::max(1, h->num_cus);
+            if (blocks <= 0) blocks = std::max(1, cus - xblocks);
             const int per_block = std::max(1, sts::cg_fit_series_per_block(p, q, I));
             const int64_t need = (N + per_block - 1) / per_block;
             if (blocks > need) blocks = (int)need;
+            if (xblocks > 0) {
+                RCCHK(h, h->xring.ensure(sts::kExpressRingBytes), "workspace");
+                RCCHK(h, h->xready.ensure(sts::kExpressReadyBytes), "workspace");
+                HIPCHK(h, hipMemsetAsync(h->xready.ptr, 0, sts::kExpressReadyBytes, s));
+            }
             h->last_grid = blocks;
+            h->last_express = xblocks;
             RCCHK(h, sts::launch_cg_fit(y, ldn, n, N, p, q, I, h->smear, init, init_status, d_coef, d_ll, d_status,
-                                        d_neval, d_ngrad, d_flags, h->ctl.as<unsigned long long>(), blocks, s),
+                                        d_neval, d_ngrad, d_flags, h->ctl.as<unsigned long long>(), blocks, xblocks,
+                                        h->xring.as<unsigned char>(), h->xready.as<unsigned>(), s),
                   "cg_fit");
         }
         HIPCHK(h, hipEventRecord(h->ev[3], s));
@@ -316,6 +330,7 @@ static int fit_device_locked(arima_handle *h, const double *d_series, int64_t N,
     ps.user_init = d_user_init != nullptr;
     ps.cg = !ps.ar_only && method == ARIMA_METHOD_CSS_CGD && k > 0;
     ps.grid = h->last_grid;
+    ps.express = h->last_express;
     ps.valid = true;
     return ARIMA_OK;
 }
@@ -345,6 +360,10 @@ static void finish_stats(arima_handle *h) {
     st.spec_hits = (int64_t)c[7];
     st.wave_multi_passes = (int64_t)c[8];
     st.spec_chains = (int64_t)c[9];
+    st.express_series = (int64_t)c[23];
+    st.express_f_passes = (int64_t)c[24];
+    st.express_g_passes = (int64_t)c[25];
+    st.express_blocks = ps.express;
     // STS_TIMING builds: F-pass, G-pass, advance, select cycles (summed over waves), kernel span, drained time
     st.diag[0] = (int64_t)c[10];
     st.diag[1] = (int64_t)c[11];

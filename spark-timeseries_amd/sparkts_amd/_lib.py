@@ -59,6 +59,8 @@ class FitStats(ctypes.Structure):
                 ("ms_cg_fit", ctypes.c_double), ("ms_total", ctypes.c_double),
                 ("wave_f_passes", ctypes.c_int64), ("wave_g_passes", ctypes.c_int64), ("grid_blocks", ctypes.c_int64),
                 ("spec_hits", ctypes.c_int64), ("wave_multi_passes", ctypes.c_int64), ("spec_chains", ctypes.c_int64),
+                ("express_blocks", ctypes.c_int64), ("express_series", ctypes.c_int64),
+                ("express_f_passes", ctypes.c_int64), ("express_g_passes", ctypes.c_int64),
                 ("diag", ctypes.c_int64 * 6)]
 
     def as_dict(self):

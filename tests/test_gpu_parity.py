@@ -293,3 +293,92 @@ def test_model_flags_near_unit_circle(engine):
     f = engine.model_flags(coef, 2, 2, True)
     exp = np.array([O.model_flags(c, 2, 2, 1) for c in coef])
     assert np.array_equal(f, exp), np.nonzero(f != exp)
+
+
+# ---- generator parity: ARIMAModel.sample / addTimeDependentEffects (ARIMA.scala:629-678) on identical noise ----
+_M32 = 0xFFFFFFFF
+
+
+def _philox4x32_10(ctr, k0, k1):
+    c = list(ctr)
+    for _ in range(10):
+        p0, p1 = 0xD2511F53 * c[0], 0xCD9E8D57 * c[2]
+        c = [((p1 >> 32) ^ c[1] ^ k0) & _M32, p1 & _M32, ((p0 >> 32) ^ c[3] ^ k1) & _M32, p0 & _M32]
+        k0, k1 = (k0 + 0x9E3779B9) & _M32, (k1 + 0xBB67AE85) & _M32
+    return c
+
+
+def _u01_53(a, b):
+    return (float(a >> 5) * 67108864.0 + float(b >> 6)) * (1.0 / 9007199254740992.0)
+
+
+def _roots_ok(poly):                       # the sampler's Schur-Cohn test, same operations (arima_kernels.hip)
+    a = list(poly)
+    for mm in range(len(a) - 1, 0, -1):
+        kk = a[mm]
+        if not abs(kk) < 1.0:
+            return False
+        den = 1.0 - kk * kk
+        a = [(a[i] - kk * a[mm - i]) / den for i in range(mm)] + a[mm:]
+    return True
+
+
+def _sampler_coef(gsid, seed, p, q, I, base, jitter):
+    """Restates k_sample's per-series coefficient draw (Philox4x32-10, redraw until stationary and invertible)."""
+    K = I + p + q
+    k0, k1 = seed & _M32, seed >> 32
+    for attempt in range(16):
+        trial = [0.0] * K
+        for j in range(0, K, 2):
+            o = _philox4x32_10([j, gsid & _M32, gsid >> 32, 0x5A17 + attempt], k0 ^ 0x3C6EF372, k1 ^ 0xA54FF53A)
+            trial[j] = base[j] + jitter * (2.0 * _u01_53(o[0], o[1]) - 1.0)
+            if j + 1 < K:
+                trial[j + 1] = base[j + 1] + jitter * (2.0 * _u01_53(o[2], o[3]) - 1.0)
+        if _roots_ok([1.0] + [-1.0 * x for x in trial[I:I + p]]) and _roots_ok([1.0] + trial[I + p:]):
+            return np.array(trial)
+    return np.array(base, dtype=np.float64)
+
+
+@pytest.mark.parametrize("pdqi", [(2, 1, 2, 1), (1, 0, 1, 1), (3, 2, 1, 0), (5, 1, 5, 1)])
+def test_sampler_filter_matches_oracle_on_identical_noise(engine, pdqi):
+    # the device generator = Philox noise -> addTimeDependentEffects (ARIMA.scala:629-646) -> inverse differencing;
+    # with (0,0,0) and no intercept it returns the noise itself, which lets the oracle filter the SAME noise
+    p, d, q, I = pdqi
+    N, T, seed, first = 48, 333, 4242, 1000
+    base = [0.5, 0.3, -0.2, 0.1, 0.05, -0.05, 0.2, 0.1, -0.1, 0.05, 0.05][: I + p + q]
+    noise = _device_sample(engine, N, T, 0, 0, 0, 0, [0.0], 0.0, seed, first).cpu().numpy()
+    out = _device_sample(engine, N, T, p, d, q, I, base, 0.02, seed, first).cpu().numpy()
+    for i in range(N):
+        c = _sampler_coef(first + i, seed, p, q, I, base, 0.02)
+        exp = O.add_time_dependent_effects(noise[i], p, d, q, I, c)
+        assert _same(out[i], exp), (i, np.max(np.abs(out[i] - exp)))
+
+
+@pytest.mark.parametrize("xblocks", [0, 4])
+def test_express_path_is_transparent(engine, xblocks):
+    # k_cg_fit hands long-running series to express workgroups (wave-per-series, row in LDS; DESIGN.md 4): results
+    # and counters must be identical with and without them, and identical to the oracle
+    N, T = 1024, 1024
+    s = _device_sample(engine, N, T, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 777).cpu().numpy()
+    engine.set_option("express_blocks", xblocks)
+    try:
+        res = engine.fit_batch(s, 2, 1, 2, True)
+        st = engine.stats()
+    finally:
+        engine.set_option("express_blocks", -1)
+    if xblocks:
+        assert st["express_blocks"] == xblocks
+    st_o, coef, ll, cnt = O.fit_batch(s, 2, 1, 2, 1)
+    exp = dict(status=st_o, coef=coef, ll=ll, n_eval=cnt[:, 0], n_grad=cnt[:, 1],
+               flags=np.array([O.model_flags(coef[i], 2, 2, 1) if st_o[i] == 0 else 0 for i in range(N)]))
+    check_fit(res, exp, f"express_blocks={xblocks}")
+
+
+def test_long_fits_through_express(engine):
+    # ARIMA(5,1,5)+c (C4's model) at T=512: many fits run thousands of evaluations (MaxEval failures included),
+    # so most of them are donated to the express path
+    meta, arr = load_case("c4_515_T512")
+    res = engine.fit_batch(arr["series"], 5, 1, 5, True)
+    st = engine.stats()
+    check_fit(res, arr, "c4_515_T512")
+    assert st["express_series"] > 0, st

@@ -46,6 +46,19 @@ def main():
                              mean_after_drain_ms=dg[5] / waves / clk * 1e3)
     nev = outs[3].cpu()
     out["n_eval_max"] = int(nev.max())
+    if dg[0] > 0:            # STS_TIMING build: ll = finish time (100 MHz counter), flags = 1 bulk / 2 express
+        import numpy as np
+        fin = outs[1].cpu().numpy()
+        path = outs[5].cpu().numpy()
+        ne = nev.numpy()
+        t0 = fin.min()
+        ms = (fin - t0) / 1e5
+        order = np.argsort(-ne)[:20]
+        out["slowest_series"] = [dict(n_eval=int(ne[i]), finish_ms=float(ms[i]), path=int(path[i])) for i in order]
+        out["latest_finishers"] = [dict(n_eval=int(ne[i]), finish_ms=float(ms[i]), path=int(path[i]))
+                                   for i in np.argsort(-ms)[:20]]
+        out["finish_ms_quantiles"] = {str(qq): float(np.quantile(ms, qq)) for qq in (0.5, 0.9, 0.99, 0.999, 1.0)}
+        out["express_count"] = int((path == 2).sum())
     out["n_eval_p999"] = float(nev.double().quantile(0.999)) if N <= 1 << 24 else None
     print(json.dumps(out))
 
