@@ -87,6 +87,9 @@ typedef struct arima_fit_stats {
     int64_t express_series;  /* series finished on the express path                                    */
     int64_t express_f_passes; /* objective / gradient passes run on the express path                    */
     int64_t express_g_passes;
+    int64_t fault;           /* != 0: the fit kernel's hand-off watchdog fired (1 = stall, 2 = lost request);
+                                the call also returns ARIMA_E_DEVICE from arima_synchronize / blocking entry points */
+    int64_t fault_info[5];   /* the kernel's record of the first fault (ticket, fills, bulk waves done, ...)      */
     int64_t diag[6];         /* diagnostics of builds with -DSTS_TIMING; else 0                       */
 } arima_fit_stats;
 

@@ -413,7 +413,8 @@ __device__ __forceinline__ void grad_column_lds(const double *row, int n,
 // series and re-transformed by the already-known reflections (same ops, same order per element). Two passes
 // per column: (1) xNormSqr -> rDiag[s] = a_s, v_s[s] = x_s[s] - a_s; (2) alpha_{s,c} for c > s and the
 // Q^T y dot product of Solver.solve (which only needs reflection s). Row s itself (the only row whose v
-// differs) is generated by random access; rows s+1.. are streamed. The upper triangle of R and the top of
+// differs) is generated by random access; rows s+1.. are streamed. An intercept column of ones needs no norm pass
+// (its sum of squares is the row count, exactly). The upper triangle of R and the top of
 // Q^T y come from re-transforming rows 0..C-1 once more. Back-substitution as Solver.solve.
 //
 // Gen provides: row_at(r, x, y) (random access), begin(r) (prime the sliding window for streaming from row r),
@@ -455,7 +456,11 @@ __device__ __forceinline__ int ols_stage(Gen &gen, const double *__restrict__ ro
         hh_apply<C>(H, S, xs, ys);
         const double xss = xs[S];
         double xnorm = 0.0 + xss * xss;
-        if (S + 1 < R) {
+        if constexpr (S == 0 && Gen::kOnesFirst) {
+            // column 0 is the intercept's 1.0 in every row: the sequential sum of R ones is R exactly (R < 2^53),
+            // so this pass needs no stream
+            xnorm = (double)R;
+        } else if (S + 1 < R) {
             gen.begin(S + 1);
             stream_elems<2>(row, gen.first_elem(S + 1), n, [&](double v) {
                 double x[C], y;
@@ -537,6 +542,7 @@ __device__ __forceinline__ int stream_ols(Gen &gen, const double *__restrict__ r
 template <int m, int INTERCEPT>
 struct ARGen {
     static constexpr int C = INTERCEPT + m;
+    static constexpr bool kOnesFirst = INTERCEPT != 0;       // column 0 = the intercept's ones
     const double *__restrict__ y;
     double w[m + 1];
     __device__ __forceinline__ void row_at(int r, double (&x)[C], double &yv) const {
@@ -573,6 +579,7 @@ struct HRGen {
     static constexpr int m = M + 1;
     static constexpr int C = I + P + Q;
     static constexpr int QA = Q > 0 ? Q : 1;
+    static constexpr bool kOnesFirst = I != 0;
     const double *__restrict__ y;
     double a[m];
     double c;

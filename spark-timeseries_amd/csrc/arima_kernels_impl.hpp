@@ -181,7 +181,21 @@ template <int K>
 struct FitSlotCore {
     CGLane<K, spec_ns<K>(), spec_nc<K>()> s;
     int64_t sid;                    // series of the slot, -1 = empty
+#ifdef STS_TIMING
+    double t_start, t_donate;       // diagnostics build only: pick-up and hand-off times (100 MHz counter)
+#endif
 };
+
+// diagnostics build only: coef[0] / coef[1] of a finished series = its pick-up / hand-off time
+template <int K>
+__device__ __forceinline__ void timing_stamp(const FitSlotCore<K> &S, double *coef_out) {
+#ifdef STS_TIMING
+    if constexpr (K >= 2) {
+        coef_out[S.sid * K + 0] = S.t_start;
+        coef_out[S.sid * K + 1] = S.t_donate;
+    }
+#endif
+}
 template <int K>
 struct alignas(8) FitSlot {
     static constexpr int kWords = (int)((sizeof(FitSlotCore<K>) + 7) / 8);
@@ -191,7 +205,10 @@ struct alignas(8) FitSlot {
 };
 
 constexpr int kFitWaves = 4;                 // waves per workgroup (one per SIMD)
-constexpr int kOldEvals = 128;               // evaluations after which a series is served with priority
+#ifndef STS_OLD_EVALS
+#define STS_OLD_EVALS 128
+#endif
+constexpr int kOldEvals = STS_OLD_EVALS;     // evaluations after which a series is served with priority
 constexpr int kFitLdsBudget = 160 * 1024 - 1024;
 // slots per wave: as many as the LDS holds, at most 2 per lane, a multiple of 8, at least 64
 template <int K>
@@ -208,17 +225,25 @@ constexpr int fit_slots_per_wave() {
 // grid) instead give a long-running series a whole wave: the row is staged once into LDS, objective passes run
 // the request's point and its predicted points on separate lanes, and gradient passes split dEdTheta's columns
 // over lanes — a pass then costs about one chain of instructions. Hand-off: an idle express wave takes a ticket
-// (ctl[20]); a bulk wave that sees an unserved ticket donates its oldest slot with >= kDonateEvals evaluations
-// into the ring entry of the next fill index (ctl[21]) and publishes it (release, then the entry's ready word =
-// index + 1); the express wave polls its entry's ready word (acquire). Express waves exit once every bulk wave has
+// (ctl[20]); a bulk wave that sees an unserved ticket claims the next fill index (ctl[21], by compare-and-swap and
+// only while it is below the ticket count), donates its oldest slot with >= kDonateEvals evaluations into that ring
+// entry and publishes it (release, then the entry's ready word = index + 1); the express wave polls its entry's
+// ready word (acquire). Express waves exit once every bulk wave has
 // finished (ctl[22]) and no fill is left for their ticket, so they never hold up the launch.
-constexpr int kExpressRing = 2048;           // ring entries (>= express waves + bulk waves: no entry is overwritten live)
+// Ring: a fill index is only claimed while a ticket is waiting for it (fill < tickets, CAS below) and is never
+// reused within a launch (fills stop at kExpressRing; a launch hands off a few thousand series at most in practice):
+// a reused entry's lines can survive, stale, in the reading XCD's L2 from the previous round (observed on MI355X:
+// an entry's tag read stale for 20 s while its ready word had moved on).
+constexpr int kExpressRing = kExpressRingEntries;
 constexpr int kExpressEntryBytes = 512;      // ring stride reserved per entry (>= sizeof(FitSlotCore<K>) for K <= 11)
 #ifndef STS_EXPRESS_GROUPS
 #define STS_EXPRESS_GROUPS 2
 #endif
 constexpr int kExpressGroups = STS_EXPRESS_GROUPS;   // series per express wave (at most; LDS permitting)
-constexpr int kDonateEvals = 256;            // a slot is donated only after this many evaluations ...
+#ifndef STS_DONATE_EVALS
+#define STS_DONATE_EVALS 256
+#endif
+constexpr int kDonateEvals = STS_DONATE_EVALS;   // a slot is donated only after this many evaluations ...
 constexpr int kDonateEvalsDrained = 32;      // ... or this many once the batch's work counter has run out
 
 template <int K>
@@ -234,13 +259,59 @@ __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Ring entry = the slot's state words + a tag word (the fill index + 1) in the entry's last 8 bytes. Entry words
+// move with agent-scope atomic stores / loads (coherent across the XCDs' L2s whatever the fences do); the reader
+// accepts an entry only when both its ready word and its tag carry its ticket.
+constexpr int kExpressTagWord = kExpressEntryBytes / 8 - 1;
+
+// Every word shared between workgroups of a launch is accessed as a GLOBAL (address space 1) agent-scope access,
+// never flat (a flat load can keep hitting this CU's stale L1 line; cdna_hip_programming.md Guideline 16).
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned gu32;
+__device__ __forceinline__ unsigned long long ld_agent(const unsigned long long *p) {
+    return __hip_atomic_load((const gu64 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned ld_agent(const unsigned *p) {
+    return __hip_atomic_load((const gu32 *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_store((gu64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(unsigned *p, unsigned v) {
+    __hip_atomic_store((gu32 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// memory-side read (an atomic RMW that changes nothing): never served by a possibly stale cache line
+__device__ __forceinline__ unsigned long long rd_fresh(const unsigned long long *p) {
+    return __hip_atomic_fetch_or((gu64 *)p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned rd_fresh(const unsigned *p) {
+    return __hip_atomic_fetch_or((gu32 *)p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long add_agent(unsigned long long *p, unsigned long long v) {
+    return __hip_atomic_fetch_add((gu64 *)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// returns the value found (== expected on success)
+__device__ __forceinline__ unsigned long long cas_agent(unsigned long long *p, unsigned long long expected,
+                                                        unsigned long long desired) {
+    __hip_atomic_compare_exchange_strong((gu64 *)p, &expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    return expected;
+}
+// agent acquire whose L1 invalidate has completed before any later load issues (the fence alone is asynchronous)
+__device__ __forceinline__ void acquire_agent() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <int K>
-__device__ __forceinline__ void copy_core(FitSlotCore<K> *dst, const FitSlotCore<K> *src, int lane) {
+__device__ __forceinline__ void publish_core(unsigned long long *dst, const FitSlotCore<K> *src, int lane,
+                                             unsigned long long tag) {
     static_assert(sizeof(FitSlotCore<K>) % 8 == 0, "8-byte words");
+    static_assert(sizeof(FitSlotCore<K>) / 8 <= kExpressTagWord, "entry + tag");
     constexpr int W = (int)(sizeof(FitSlotCore<K>) / 8);
     const unsigned long long *s = reinterpret_cast<const unsigned long long *>(src);
-    unsigned long long *d = reinterpret_cast<unsigned long long *>(dst);
-    for (int w = lane; w < W; w += 64) d[w] = s[w];
+    for (int w = lane; w < W; w += 64) st_agent(&dst[w], s[w]);
+    if (lane == 0) st_agent(&dst[kExpressTagWord], tag);
 }
 
 // Express wave: up to XG long series at once, one per group of 64/XG lanes (XG from the row length: each group
@@ -253,13 +324,33 @@ __device__ __forceinline__ void copy_core(FitSlotCore<K> *dst, const FitSlotCore
 template <int K>
 constexpr int express_group_bytes(int n) { return express_state_bytes<K>() + ((n + 1) & ~1) * 8 + 16 * 8; }
 
+// Hand-off watchdog: a persistent kernel must never spin forever. A waiting group that sees none of the launch's
+// progress counters move for kWatchdogTicks (100 MHz real-time counter) gives up, and a fitting group whose state
+// posts no request without being finished is dropped; either records the first fault in ctl[26..31] (the host
+// reports it as a device error) and the wave drains normally.
+constexpr unsigned long long kWatchdogTicks = 2000000000ull;    // 20 s without any progress of the launch
+enum : unsigned long long { FAULT_HANDOFF_STALL = 1, FAULT_NO_REQUEST = 2 };
+
+__device__ __forceinline__ void record_fault(unsigned long long *ctl, unsigned long long code, unsigned long long a,
+                                             unsigned long long b, unsigned long long c, unsigned long long d,
+                                             unsigned long long e) {
+    if (cas_agent(&ctl[26], 0ull, code) == 0ull) {
+        st_agent(&ctl[27], a);
+        st_agent(&ctl[28], b);
+        st_agent(&ctl[29], c);
+        st_agent(&ctl[30], d);
+        st_agent(&ctl[31], e);
+    }
+}
+
+
 template <int P, int Q, int I, bool SMEAR>
 __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__restrict__ y, int64_t ld, int n,
                             double *__restrict__ coef_out, double *__restrict__ ll_out,
                             int32_t *__restrict__ status_out, int32_t *__restrict__ n_eval_out,
                             int32_t *__restrict__ n_grad_out, uint8_t *__restrict__ flags_out,
                             unsigned long long *__restrict__ ctl, unsigned char *__restrict__ xq,
-                            unsigned *__restrict__ xready, unsigned long long bulk_waves, int lane) {
+                            unsigned *__restrict__ xready, int64_t N, int lane) {
     constexpr int K = I + P + Q;
     constexpr int NS = spec_ns<K>();
     const int gbytes = express_group_bytes<K>(n);
@@ -276,37 +367,71 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
     // group state: 0 = waiting on ticket, 1 = fitting, 2 = retired (wave-uniform per group after each shfl)
     int gstate = 0;
     unsigned long long ticket = 0;
-    if (glead) ticket = atomicAdd(&ctl[20], 1ull);
+    unsigned long long wd_sig = 0, wd_t = 0;                // watchdog (group leaders)
+    unsigned wd_polls = 0;
+    unsigned long long tk_time = 0, tk_polls = 0;          // fault diagnostics: this ticket's age and polls,
+    unsigned tk_rfirst = 0, tk_rmax = 0;                    // first / largest ready word seen
+    if (glead) {
+        ticket = add_agent(&ctl[20], 1ull);
+        tk_time = __builtin_amdgcn_s_memrealtime();
+    }
     ticket = __shfl(ticket, grp * GL);
     for (;;) {
         // ---- groups waiting on a ticket: poll (group leader), then load the entry (whole group) ----
         int arrived = 0;
         if (gstate == 0 && glead) {
             const unsigned e = (unsigned)(ticket % kExpressRing);
-            unsigned r = __hip_atomic_load(&xready[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (r == (unsigned)(ticket + 1)) {
-                arrived = 1;
+            const unsigned long long *ent = reinterpret_cast<const unsigned long long *>(xq + (size_t)e * kExpressEntryBytes);
+            // poll the ready word; every 32nd poll reads it at the memory side
+            unsigned r = (tk_polls & 31u) == 31u ? rd_fresh(&xready[e]) : ld_agent(&xready[e]);
+            if (tk_polls++ == 0) tk_rfirst = r;
+            tk_rmax = r > tk_rmax ? r : tk_rmax;
+            if (ticket >= (unsigned long long)kExpressRing) {
+                arrived = 2;                                // beyond the ring: never filled
+            } else if (r == (unsigned)(ticket + 1)) {
+                arrived = rd_fresh(&ent[kExpressTagWord]) == ticket + 1 ? 1 : 0;
             } else {
-                const unsigned long long bd = __hip_atomic_load(&ctl[22], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (bd >= bulk_waves) {                     // every fill has happened
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    const unsigned long long fl =
-                        __hip_atomic_load(&ctl[21], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    r = __hip_atomic_load(&xready[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    arrived = (r == (unsigned)(ticket + 1)) ? 1 : (ticket >= fl ? 2 : 0);
+                // every fill has happened once the work counter has run out and every bulk wave that started has
+                // finished (a bulk wave starting later gets no series, so it cannot fill): no dependence on bulk
+                // workgroups that are not resident yet, so concurrent launches cannot deadlock
+                if (ld_agent(&ctl[0]) >= (unsigned long long)N) {
+                    acquire_agent();
+                    const unsigned long long bd = ld_agent(&ctl[22]);
+                    const unsigned long long bs = ld_agent(&ctl[17]);
+                    if (bd == bs) {
+                        acquire_agent();
+                        const unsigned long long fl = ld_agent(&ctl[21]);
+                        r = rd_fresh(&xready[e]);
+                        if (r == (unsigned)(ticket + 1)) arrived = rd_fresh(&ent[kExpressTagWord]) == ticket + 1 ? 1 : 0;
+                        else arrived = ticket >= fl ? 2 : 0;
+                    }
                 }
             }
-            if (arrived == 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            if (arrived == 0 && (++wd_polls & 255u) == 0u) {
+                const unsigned long long sig = ld_agent(&ctl[0]) + ld_agent(&ctl[17]) + ld_agent(&ctl[20]) +
+                                               ld_agent(&ctl[21]) + ld_agent(&ctl[22]);
+                const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+                if (sig != wd_sig || wd_t == 0) {
+                    wd_sig = sig;
+                    wd_t = now;
+                } else if (now - wd_t > kWatchdogTicks) {
+                    record_fault(ctl, FAULT_HANDOFF_STALL, ticket, ld_agent(&ctl[21]) | (ld_agent(&ctl[20]) << 32),
+                                 tk_polls | (((now - tk_time) / 100000ull) << 32),
+                                 (unsigned long long)tk_rmax | ((unsigned long long)tk_rfirst << 32),
+                                 (unsigned long long)r | ((unsigned long long)e << 32));
+                    arrived = 2;
+                }
+            }
+            if (arrived == 1) acquire_agent();
         }
         arrived = __shfl(arrived, grp * GL);
         if (arrived == 2) gstate = 2;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (arrived == 1) {
             const unsigned e = (unsigned)(ticket % kExpressRing);
-            const FitSlotCore<K> *src = reinterpret_cast<const FitSlotCore<K> *>(xq + (size_t)e * kExpressEntryBytes);
+            const unsigned long long *src = reinterpret_cast<const unsigned long long *>(xq + (size_t)e * kExpressEntryBytes);
             constexpr int W = (int)(sizeof(FitSlotCore<K>) / 8);
-            for (int w = gl; w < W; w += GL)
-                reinterpret_cast<unsigned long long *>(&ES)[w] = reinterpret_cast<const unsigned long long *>(src)[w];
+            for (int w = gl; w < W; w += GL) reinterpret_cast<unsigned long long *>(&ES)[w] = rd_fresh(&src[w]);
         }
         wave_sync_lds();
         if (arrived == 1) {
@@ -323,6 +448,12 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
         }
         // ---- one pass for every group: the objective pass when all groups want F; otherwise the gradient pass,
         //      whose lanes in F groups evaluate their chain points (the pass also yields the objective) ----
+        if (gstate == 1 && ES.s.req == REQ_NONE && !ES.s.done()) {     // invariant broken: drop, never spin
+            if (glead)
+                record_fault(ctl, FAULT_NO_REQUEST, ticket, (unsigned long long)ES.sid, ES.s.pc,
+                             ((unsigned long long)ES.s.status << 16) | ES.s.n_eval, ld_agent(&ctl[21]));
+            gstate = 2;
+        }
         const int req = gstate == 1 ? (int)ES.s.req : REQ_NONE;
         const int nsp = req == REQ_F ? (int)ES.s.rq_nspec : 0;
         double c[K];
@@ -366,10 +497,14 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
             write_fit<K>(ES.sid, ES.s.status, pt, ES.s.prev_obj, ES.s.n_eval, ES.s.n_grad,
                          ES.s.status == ARIMA_ST_OK ? model_flags<P, Q, I>(pt) : (uint8_t)0, coef_out, ll_out,
                          status_out, n_eval_out, n_grad_out, flags_out, 2);
+            timing_stamp<K>(ES, coef_out);
             evals += ES.s.n_eval;
             grads += ES.s.n_grad;
             hits += ES.s.spec_hits;
-            ticket = atomicAdd(&ctl[20], 1ull);
+            ticket = add_agent(&ctl[20], 1ull);
+            tk_time = __builtin_amdgcn_s_memrealtime();
+            tk_polls = 0;
+            tk_rfirst = tk_rmax = 0;
         }
         if (fin) gstate = 0;
         ticket = __shfl(ticket, grp * GL);
@@ -391,16 +526,18 @@ __global__ __launch_bounds__(64 * kFitWaves, 1) void k_cg_fit(
     const int32_t *__restrict__ init_status, double *__restrict__ coef_out, double *__restrict__ ll_out,
     int32_t *__restrict__ status_out, int32_t *__restrict__ n_eval_out, int32_t *__restrict__ n_grad_out,
     uint8_t *__restrict__ flags_out, unsigned long long *__restrict__ ctl, unsigned char *__restrict__ xq,
-    unsigned *__restrict__ xready, int n_bulk) {
+    unsigned *__restrict__ xready, int n_bulk, int join_express) {
     // ctl[0] = work counter, ctl[1] = lane F passes, ctl[2] = lane G passes, ctl[3] = wave F passes (one chain),
     // ctl[4] = wave G passes, ctl[5] = objective evaluations, ctl[6] = gradient evaluations, ctl[7] = spec hits,
     // ctl[8] = wave F passes with speculative chains, ctl[9] = speculative chains evaluated,
-    // ctl[20] = express tickets, ctl[21] = express fills (donations), ctl[22] = bulk waves finished,
+    // ctl[17] = bulk waves started, ctl[20] = express tickets, ctl[21] = express fills (donations),
+    // ctl[22] = bulk waves finished,
     // ctl[23] = series finished on the express path, ctl[24] / ctl[25] = express F / G passes
     constexpr int K = I + P + Q;
     constexpr int NS = spec_ns<K>();
     constexpr int NJ = (SPW + 63) / 64;      // slot groups: lane l owns slots l, l + 64, ...
     static_assert(SPW >= 64 && SPW <= 128, "slots per wave");
+    static_assert(sizeof(FitSlotCore<K>) <= kExpressEntryBytes, "express ring entry");
     __shared__ FitSlot<K> slots[kFitWaves][SPW];
     __shared__ int assign[kFitWaves][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -408,8 +545,13 @@ __global__ __launch_bounds__(64 * kFitWaves, 1) void k_cg_fit(
     if ((int)blockIdx.x >= n_bulk) {                      // express workgroup: this wave's share of the LDS
         fit_express<P, Q, I, SMEAR>(reinterpret_cast<unsigned char *>(&slots[wave][0]), (int)sizeof(slots[0]), y, ld,
                                     n, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out, ctl, xq,
-                                    xready, (unsigned long long)n_bulk * kFitWaves, lane);
+                                    xready, N, lane);
         return;
+    }
+    if (has_express && lane == 0) {                       // counted before this wave takes any series (release)
+        add_agent(&ctl[17], 1ull);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     FitSlot<K> *ws = slots[wave];
     unsigned long long lane_f = 0, lane_g = 0, wave_f = 0, wave_g = 0, wave_m = 0, evals = 0, grads = 0, hits = 0,
@@ -434,7 +576,7 @@ __global__ __launch_bounds__(64 * kFitWaves, 1) void k_cg_fit(
             if (m == 0ull) break;
             const int leader = __ffsll((long long)m) - 1;
             unsigned long long base = 0;
-            if (lane == leader) base = atomicAdd(&ctl[0], (unsigned long long)__popcll(m));
+            if (lane == leader) base = add_agent(&ctl[0], (unsigned long long)__popcll(m));
             base = __shfl(base, leader);
             if (need) {
                 const int rank = __popcll(m & ((1ull << lane) - 1ull));
@@ -464,6 +606,10 @@ __global__ __launch_bounds__(64 * kFitWaves, 1) void k_cg_fit(
                             g0[j] = 0.0;
                         }
                         S.sid = sid;
+#ifdef STS_TIMING
+                        S.t_start = (double)__builtin_amdgcn_s_memrealtime();
+                        S.t_donate = 0.0;
+#endif
                         S.s.start(x0);
                         S.s.advance(0.0, g0);           // posts the first request: G at the initial point
                         need = false;
@@ -615,6 +761,7 @@ __global__ __launch_bounds__(64 * kFitWaves, 1) void k_cg_fit(
                 write_fit<K>(S.sid, S.s.status, pt, S.s.prev_obj, S.s.n_eval, S.s.n_grad,
                              S.s.status == ARIMA_ST_OK ? model_flags<P, Q, I>(pt) : (uint8_t)0, coef_out, ll_out,
                              status_out, n_eval_out, n_grad_out, flags_out);
+                timing_stamp<K>(S, coef_out);
                 evals += S.s.n_eval;
                 grads += S.s.n_grad;
                 hits += S.s.spec_hits;
@@ -626,12 +773,12 @@ __global__ __launch_bounds__(64 * kFitWaves, 1) void k_cg_fit(
             // an express wave is waiting: hand it this wave's oldest slot (the likely critical path)
             unsigned long long wants = 0, filled = 0;
             if (lane0) {
-                wants = __hip_atomic_load(&ctl[20], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                filled = __hip_atomic_load(&ctl[21], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                wants = ld_agent(&ctl[20]);
+                filled = ld_agent(&ctl[21]);
             }
             wants = __shfl(wants, 0);
             filled = __shfl(filled, 0);
-            if (wants > filled) {
+            if (wants > filled && filled < (unsigned long long)kExpressRing) {
                 const int donate_min = __any(drained) ? kDonateEvalsDrained : kDonateEvals;
                 unsigned long long key = 0;
 #pragma unroll
@@ -648,19 +795,38 @@ __global__ __launch_bounds__(64 * kFitWaves, 1) void k_cg_fit(
                     const unsigned long long o = __shfl_xor(key, off);
                     key = o > key ? o : key;
                 }
-                if (key) {
-                    const int bs = (int)(key & 0xffffull) - 1;
-                    unsigned long long jx = 0;
-                    if (lane0) jx = atomicAdd(&ctl[21], 1ull);
-                    jx = __shfl(jx, 0);
-                    const unsigned e = (unsigned)(jx % kExpressRing);
-                    copy_core<K>(reinterpret_cast<FitSlotCore<K> *>(xq + (size_t)e * kExpressEntryBytes), &ws[bs].c, lane);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    if (lane0) {
-                        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        __hip_atomic_store(&xready[e], (unsigned)(jx + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // claim a fill index that a waiting ticket will read: never beyond the tickets (an unbounded
+                // fill could overwrite a ring entry before its ticket holder has read it)
+                unsigned long long jx = 0;
+                int claimed = 0;
+                if (lane0 && key) {
+                    unsigned long long f = filled;
+                    while (f < wants && f < (unsigned long long)kExpressRing) {
+                        const unsigned long long prev = cas_agent(&ctl[21], f, f + 1ull);
+                        if (prev == f) {
+                            jx = f;
+                            claimed = 1;
+                            break;
+                        }
+                        f = prev;
+                        wants = ld_agent(&ctl[20]);
                     }
+                }
+                claimed = __shfl(claimed, 0);
+                jx = __shfl(jx, 0);
+                if (claimed) {
+                    const int bs = (int)(key & 0xffffull) - 1;
+                    const unsigned e = (unsigned)(jx % kExpressRing);
+#ifdef STS_TIMING
+                    if (lane == (bs & 63)) ws[bs].c.t_donate = (double)__builtin_amdgcn_s_memrealtime();
+                    wave_sync_lds();
+#endif
+                    publish_core<K>(reinterpret_cast<unsigned long long *>(xq + (size_t)e * kExpressEntryBytes), &ws[bs].c,
+                                    lane, jx + 1);
+                    // the entry went out write-through (sc1): drain this wave's stores, then the flag (no L2
+                    // write-back needed; cdna_hip_programming.md Guideline 16, R1)
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if (lane0) st_agent(&xready[e], (unsigned)(jx + 1));
                     if (lane == (bs & 63)) {
                         ws[bs].c.sid = -1;
                         ws[bs].c.s.req = REQ_NONE;
@@ -678,14 +844,17 @@ __global__ __launch_bounds__(64 * kFitWaves, 1) void k_cg_fit(
         if (lane0) {                                        // this bulk wave will fill no more express entries
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            atomicAdd(&ctl[22], 1ull);
+            add_agent(&ctl[22], 1ull);
         }
-        // its slots are all finished: the wave serves the remaining long series on the express path, in the LDS
-        // share its slots used
-        wave_sync_lds();
-        fit_express<P, Q, I, SMEAR>(reinterpret_cast<unsigned char *>(&slots[wave][0]), (int)sizeof(slots[0]), y, ld,
-                                    n, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out, ctl, xq,
-                                    xready, (unsigned long long)n_bulk * kFitWaves, lane);
+        // its slots are all finished: unless the launch shares the GPU with other fits (join_express = 0: the
+        // workgroup should exit and make room), the wave serves the remaining long series on the express path,
+        // in the LDS share its slots used
+        if (join_express) {
+            wave_sync_lds();
+            fit_express<P, Q, I, SMEAR>(reinterpret_cast<unsigned char *>(&slots[wave][0]), (int)sizeof(slots[0]), y,
+                                        ld, n, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out, ctl,
+                                        xq, xready, N, lane);
+        }
     }
 #ifdef STS_TIMING
     if (lane0) {
@@ -835,16 +1004,18 @@ int launch_ar_fit_P(const double *y, int64_t ld, int n, int64_t N, int I, double
     }
 }
 
-template <int P>
-int launch_cg_fit_P(const double *y, int64_t ld, int n, int64_t N, int q, int I, int smear, const double *init,
-                    const int32_t *init_status, double *coef_out, double *ll_out, int32_t *status_out,
-                    int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out, unsigned long long *ctl,
-                    int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready, hipStream_t s) {
+// k_cg_fit launcher for one AR order and Breeze reading (each instantiated in its own translation unit,
+// arima_cg_p<P>_s<S>.hip, so the build parallelises over the heaviest kernel)
+template <int P, bool S>
+int launch_cg_fit_PS(const double *y, int64_t ld, int n, int64_t N, int q, int I, const double *init,
+                     const int32_t *init_status, double *coef_out, double *ll_out, int32_t *status_out,
+                     int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out, unsigned long long *ctl,
+                     int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready, int join_express,
+                     hipStream_t s) {
     return with_order(q, [&](auto Qc) {
         return with_bool(I, [&](auto Ic) {
-            return with_smear(smear, [&](auto Sc) {
+            {
                 constexpr int Q = decltype(Qc)::value, II = decltype(Ic)::value;
-                constexpr bool S = decltype(Sc)::value != 0;
                 if constexpr (P + Q + II == 0) {
                     return ARIMA_E_INVALID_ARG;
                 } else {
@@ -854,12 +1025,27 @@ int launch_cg_fit_P(const double *y, int64_t ld, int n, int64_t N, int q, int I,
                     if (n > express_max_n<P + Q + II>(lds_per_wave)) express_blocks = 0;
                     hipLaunchKernelGGL((k_cg_fit<P, Q, II, S, SPW>), dim3(grid_blocks + express_blocks),
                                        dim3(64 * kFitWaves), 0, s, y, ld, n, N, init, init_status, coef_out, ll_out,
-                                       status_out, n_eval_out, n_grad_out, flags_out, ctl, xq, xready, grid_blocks);
+                                       status_out, n_eval_out, n_grad_out, flags_out, ctl, xq, xready, grid_blocks,
+                                       join_express);
                     STS_CHECK_LAUNCH();
                     return ARIMA_OK;
                 }
-            });
+            }
         });
+    });
+}
+
+template <int P>
+int launch_cg_fit_P(const double *y, int64_t ld, int n, int64_t N, int q, int I, int smear, const double *init,
+                    const int32_t *init_status, double *coef_out, double *ll_out, int32_t *status_out,
+                    int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out, unsigned long long *ctl,
+                    int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready, int join_express,
+                    hipStream_t s) {
+    return with_smear(smear, [&](auto Sc) {
+        return launch_cg_fit_PS<P, (decltype(Sc)::value != 0)>(y, ld, n, N, q, I, init, init_status, coef_out, ll_out,
+                                                               status_out, n_eval_out, n_grad_out, flags_out, ctl,
+                                                               grid_blocks, express_blocks, xq, xready, join_express,
+                                                               s);
     });
 }
 
@@ -918,7 +1104,15 @@ int launch_model_flags_P(const double *coef, int64_t N, int q, int I, uint8_t *f
     });
 }
 
+#define STS_DECLARE_CG(PP, SS, EXT)                                                                             \
+    EXT template int launch_cg_fit_PS<PP, SS>(const double *, int64_t, int, int64_t, int, int, const double *,    \
+                                              const int32_t *, double *, double *, int32_t *, int32_t *,        \
+                                              int32_t *, uint8_t *, unsigned long long *, int, int,             \
+                                              unsigned char *, unsigned *, int, hipStream_t);
+
 #define STS_DECLARE_P(PP, EXT)                                                                                  \
+    STS_DECLARE_CG(PP, false, extern)                                                                           \
+    STS_DECLARE_CG(PP, true, extern)                                                                            \
     EXT template int launch_hr_init_P<PP>(const double *, int64_t, int, int64_t, int, int, double *, int32_t *,  \
                                           hipStream_t);                                                         \
     EXT template int launch_ar_fit_P<PP>(const double *, int64_t, int, int64_t, int, double *, double *,         \
@@ -926,7 +1120,7 @@ int launch_model_flags_P(const double *coef, int64_t N, int q, int I, uint8_t *f
     EXT template int launch_cg_fit_P<PP>(const double *, int64_t, int, int64_t, int, int, int, const double *,   \
                                          const int32_t *, double *, double *, int32_t *, int32_t *, int32_t *,  \
                                          uint8_t *, unsigned long long *, int, int, unsigned char *, unsigned *, \
-                                         hipStream_t);                                                          \
+                                         int, hipStream_t);                                                     \
     EXT template int cg_fit_series_per_block_P<PP>(int, int);                                                   \
     EXT template int launch_css_loglik_P<PP>(const double *, int64_t, int, int64_t, int, int, const double *,    \
                                              double *, hipStream_t);                                            \

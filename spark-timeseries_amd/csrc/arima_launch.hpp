@@ -25,9 +25,10 @@ int launch_cg_fit(const double *y, int64_t ld, int n, int64_t N, int p, int q, i
                   const double *init, const int32_t *init_status, double *coef_out, double *ll_out,
                   int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
                   unsigned long long *ctl, int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready,
-                  hipStream_t s);
-constexpr int kExpressRingBytes = 2048 * 512;    // k_cg_fit's express hand-off ring (kExpressRing x kExpressEntryBytes)
-constexpr int kExpressReadyBytes = 2048 * 4;
+                  int join_express, hipStream_t s);
+constexpr int kExpressRingEntries = 32768;      // k_cg_fit's express hand-offs per launch (entries never reused)
+constexpr int kExpressRingBytes = kExpressRingEntries * 512;   // x kExpressEntryBytes
+constexpr int kExpressReadyBytes = kExpressRingEntries * 4;
 int launch_css_loglik(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, const double *coef,
                       double *ll_out, hipStream_t s);
 int launch_css_grad(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, int smear,

@@ -59,6 +59,25 @@ struct PendingStats {
     int64_t grid = 0, express = 0;
 };
 
+// Device workspace of one fit in flight: Hannan-Rissanen init, the fit kernel's counters and its express ring.
+struct FitWs {
+    DevBuf init, hr_status, ctl, xring, xready;
+};
+
+// One lane of the order search's concurrent fits (arima_order_search_batch*): its own stream, workspace and
+// candidate outputs. Fits of consecutive grid points run on different lanes, so the tail of one fit kernel (its
+// slowest series) overlaps the next fits; the select steps stay in grid order on the call's stream.
+struct SearchLane {
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_fit = nullptr, ev_sel = nullptr;
+    bool sel_recorded = false;
+    FitWs ws;
+    DevBuf coef, ll, status, neval, ngrad, flags;
+};
+
+constexpr int kMaxSearchLanes = 8;
+constexpr int kMaxD = 16;
+
 }  // namespace
 
 struct arima_handle {
@@ -72,17 +91,23 @@ struct arima_handle {
     std::string err;
     arima_fit_stats stats{};
     PendingStats pending;
+    bool fit_ctl = false;          // ctl_host holds (or will hold, in stream order) the last fit's kernel counters
     int smear = 1;            // Breeze 0.12 overlap semantics at ARIMA.scala:526: element-wise copy
     int grid_blocks_override = 0;
     int express_blocks = -1;       // k_cg_fit express workgroups (-1: num_cus / 16)
     int64_t last_express = 0;
     int64_t last_grid = 0;
+    int search_lanes = 4;          // concurrent fits of the order search
     // device workspaces
-    DevBuf diff, init, hr_status, ctl, xring, xready;
+    DevBuf diff;
+    FitWs ws;
     // host-API staging
     DevBuf h_series, h_coef, h_ll, h_status, h_neval, h_ngrad, h_flags, h_uinit, h_aux;
-    // order-search candidate buffers (one fit of the grid at a time) + host-API staging of its outputs
-    DevBuf os_coef, os_ll, os_status, os_neval, os_ngrad, os_flags, os_order;
+    // order search: the differenced series per d, the concurrent fit lanes, host-API staging of the orders
+    DevBuf os_diff[kMaxD + 1];
+    hipEvent_t ev_diff[kMaxD + 1] = {};
+    SearchLane lanes[kMaxSearchLanes];
+    DevBuf os_order;
     unsigned long long *ctl_host = nullptr;   // pinned
 };
 
@@ -187,6 +212,16 @@ int arima_destroy(arima_handle *h) {
     hipSetDevice(h->device);
     if (h->stream) hipStreamSynchronize(h->stream);
     if (h->has_done) hipEventSynchronize(h->ev_done);
+    for (auto &l : h->lanes) {
+        if (l.stream) {
+            hipStreamSynchronize(l.stream);
+            hipStreamDestroy(l.stream);
+        }
+        if (l.ev_fit) hipEventDestroy(l.ev_fit);
+        if (l.ev_sel) hipEventDestroy(l.ev_sel);
+    }
+    for (auto &e : h->ev_diff)
+        if (e) hipEventDestroy(e);
     for (auto &e : h->ev)
         if (e) hipEventDestroy(e);
     if (h->ev_done) hipEventDestroy(h->ev_done);
@@ -213,12 +248,24 @@ int arima_get_last_stats(const arima_handle *hc, arima_fit_stats *out) {
     return ARIMA_OK;
 }
 
+// The last fit's kernel recorded a watchdog fault (k_cg_fit's hand-off): its results are incomplete.
+static int check_fault(arima_handle *h) {
+    if (h->fit_ctl && h->ctl_host[26] != 0) {
+        h->fit_ctl = false;                      // reported once
+        char msg[160];
+        snprintf(msg, sizeof msg, "fit kernel watchdog fault %llu (info %llu %llu %llu %llu %llu)", h->ctl_host[26],
+                 h->ctl_host[27], h->ctl_host[28], h->ctl_host[29], h->ctl_host[30], h->ctl_host[31]);
+        return set_err(h, ARIMA_E_DEVICE, msg);
+    }
+    return ARIMA_OK;
+}
+
 int arima_synchronize(arima_handle *h) {
     if (!h) return ARIMA_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
     HIPCHK(h, hipSetDevice(h->device));
     if (h->has_done) HIPCHK(h, hipEventSynchronize(h->ev_done));
-    return ARIMA_OK;
+    return check_fault(h);
 }
 
 int arima_set_option(arima_handle *h, const char *name, int64_t value) {
@@ -227,6 +274,10 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
     if (!strcmp(name, "smear")) { h->smear = value ? 1 : 0; return ARIMA_OK; }
     if (!strcmp(name, "express_blocks")) { h->express_blocks = (int)std::max<int64_t>(-1, value); return ARIMA_OK; }
     if (!strcmp(name, "grid_blocks")) { h->grid_blocks_override = (int)std::max<int64_t>(0, value); return ARIMA_OK; }
+    if (!strcmp(name, "search_lanes")) {
+        h->search_lanes = (int)std::min<int64_t>(kMaxSearchLanes, std::max<int64_t>(1, value));
+        return ARIMA_OK;
+    }
     return set_err(h, ARIMA_E_INVALID_ARG, "unknown option");
 }
 
@@ -241,6 +292,69 @@ static hipError_t end_call(arima_handle *h, hipStream_t s) {
     hipError_t e = hipEventRecord(h->ev_done, s);
     if (e == hipSuccess) h->has_done = true;
     return e;
+}
+
+// Hannan-Rissanen init (unless user init) and the fit kernel -- or the AR-only shortcut, or a uniform per-series
+// status -- over already-differenced rows y (N x n, leading dimension ldn), on stream s with workspace ws.
+// ev_mid (optional) is recorded between the init and the fit kernel. shared_gpu: other fits run concurrently (the
+// order search's lanes), so the fit kernel's drained workgroups exit instead of joining its express pool.
+static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn, int n, int64_t N, int32_t p,
+                       int32_t q, int32_t I, int32_t method, const double *d_user_init, double *d_coef, double *d_ll,
+                       int32_t *d_status, int32_t *d_neval, int32_t *d_ngrad, uint8_t *d_flags, hipStream_t s,
+                       hipEvent_t ev_mid, int64_t *grid_out, int64_t *express_out, bool shared_gpu = false) {
+    const int k = I + p + q;
+    *grid_out = 0;
+    *express_out = 0;
+    RCCHK(h, ws.ctl.ensure(kCtlWords * sizeof(unsigned long long)), "workspace");
+    HIPCHK(h, hipMemsetAsync(ws.ctl.ptr, 0, kCtlWords * sizeof(unsigned long long), s));
+    HIPCHK(h, hipMemsetAsync(ws.ctl.as<unsigned long long>() + 15, 0xff, sizeof(unsigned long long), s));
+    if (p > 0 && q == 0) {                                     // AR-only shortcut, method never checked
+        if (ev_mid) HIPCHK(h, hipEventRecord(ev_mid, s));
+        RCCHK(h, sts::launch_ar_fit(y, ldn, n, N, p, I, d_coef, d_ll, d_status, d_neval, d_ngrad, d_flags, s),
+              "ar_fit");
+        return ARIMA_OK;
+    }
+    const double *init = d_user_init;
+    const int32_t *init_status = nullptr;
+    if (!d_user_init) {
+        RCCHK(h, ws.init.ensure((size_t)N * std::max(k, 1) * sizeof(double)), "workspace");
+        RCCHK(h, ws.hr_status.ensure((size_t)N * sizeof(int32_t)), "workspace");
+        RCCHK(h, sts::launch_hr_init(y, ldn, n, N, p, q, I, ws.init.as<double>(), ws.hr_status.as<int32_t>(), s),
+              "hr_init");
+        init = ws.init.as<double>();
+        init_status = ws.hr_status.as<int32_t>();
+    }
+    if (ev_mid) HIPCHK(h, hipEventRecord(ev_mid, s));
+    if (method != ARIMA_METHOD_CSS_CGD || k == 0) {
+        const unsigned grid = (unsigned)((N + 255) / 256);
+        const int32_t code = (method != ARIMA_METHOD_CSS_CGD) ? ARIMA_ST_UNSUPPORTED_METHOD : ARIMA_ST_ZERO_PARAMS;
+        hipLaunchKernelGGL(k_fill_status, dim3(grid), dim3(256), 0, s, N, k, init_status, code, d_coef, d_ll,
+                           d_status, d_neval, d_ngrad, d_flags);
+        HIPCHK(h, hipGetLastError());
+        return ARIMA_OK;
+    }
+    // one persistent workgroup per CU (4 waves x the kernel's optimizer slots), the last num_cus/16 of them express
+    // workgroups (k_cg_fit's long-series path); fewer bulk blocks when the batch cannot fill them
+    const int cus = std::max(1, h->num_cus);
+    int xblocks = h->express_blocks >= 0 ? h->express_blocks : std::max(1, cus / 16);
+    if (xblocks >= cus) xblocks = cus - 1;
+    int blocks = h->grid_blocks_override;
+    if (blocks <= 0) blocks = std::max(1, cus - xblocks);
+    const int per_block = std::max(1, sts::cg_fit_series_per_block(p, q, I));
+    const int64_t need = (N + per_block - 1) / per_block;
+    if (blocks > need) blocks = (int)need;
+    if (xblocks > 0) {
+        RCCHK(h, ws.xring.ensure(sts::kExpressRingBytes), "workspace");
+        RCCHK(h, ws.xready.ensure(sts::kExpressReadyBytes), "workspace");
+        HIPCHK(h, hipMemsetAsync(ws.xready.ptr, 0, sts::kExpressReadyBytes, s));
+    }
+    *grid_out = blocks;
+    *express_out = xblocks;
+    RCCHK(h, sts::launch_cg_fit(y, ldn, n, N, p, q, I, h->smear, init, init_status, d_coef, d_ll, d_status, d_neval,
+                                d_ngrad, d_flags, ws.ctl.as<unsigned long long>(), blocks, xblocks,
+                                ws.xring.as<unsigned char>(), ws.xready.as<unsigned>(), shared_gpu ? 0 : 1, s),
+          "cg_fit");
+    return ARIMA_OK;
 }
 
 static int fit_device_locked(arima_handle *h, const double *d_series, int64_t N, int32_t T, int64_t ld, int32_t p,
@@ -260,65 +374,17 @@ static int fit_device_locked(arima_handle *h, const double *d_series, int64_t N,
     begin_call(h, s);
 
     RCCHK(h, h->diff.ensure((size_t)N * ldn * sizeof(double)), "workspace");
-    RCCHK(h, h->ctl.ensure(kCtlWords * sizeof(unsigned long long)), "workspace");
-    HIPCHK(h, hipMemsetAsync(h->ctl.ptr, 0, kCtlWords * sizeof(unsigned long long), s));
-    HIPCHK(h, hipMemsetAsync(h->ctl.as<unsigned long long>() + 15, 0xff, sizeof(unsigned long long), s));
-
     HIPCHK(h, hipEventRecord(h->ev[0], s));
     RCCHK(h, sts::launch_difference(d_series, ld, h->diff.as<double>(), ldn, N, T, d, 1, s), "difference");
     HIPCHK(h, hipEventRecord(h->ev[1], s));
-    const double *y = h->diff.as<double>();
-
-    if (p > 0 && q == 0) {                                     // AR-only shortcut, method never checked
-        RCCHK(h, sts::launch_ar_fit(y, ldn, n, N, p, I, d_coef, d_ll, d_status, d_neval, d_ngrad, d_flags, s),
-              "ar_fit");
-        HIPCHK(h, hipEventRecord(h->ev[2], s));
-        HIPCHK(h, hipEventRecord(h->ev[3], s));
-    } else {
-        const double *init = d_user_init;
-        const int32_t *init_status = nullptr;
-        if (!d_user_init) {
-            RCCHK(h, h->init.ensure((size_t)N * std::max(k, 1) * sizeof(double)), "workspace");
-            RCCHK(h, h->hr_status.ensure((size_t)N * sizeof(int32_t)), "workspace");
-            RCCHK(h, sts::launch_hr_init(y, ldn, n, N, p, q, I, h->init.as<double>(), h->hr_status.as<int32_t>(), s),
-                  "hr_init");
-            init = h->init.as<double>();
-            init_status = h->hr_status.as<int32_t>();
-        }
-        HIPCHK(h, hipEventRecord(h->ev[2], s));
-        const unsigned grid = (unsigned)((N + 255) / 256);
-        if (method != ARIMA_METHOD_CSS_CGD || k == 0) {
-            const int32_t code = (method != ARIMA_METHOD_CSS_CGD) ? ARIMA_ST_UNSUPPORTED_METHOD : ARIMA_ST_ZERO_PARAMS;
-            hipLaunchKernelGGL(k_fill_status, dim3(grid), dim3(256), 0, s, N, k, init_status, code, d_coef, d_ll,
-                               d_status, d_neval, d_ngrad, d_flags);
-            HIPCHK(h, hipGetLastError());
-        } else {
-            // one persistent workgroup per CU (4 waves x the kernel's optimizer slots), the last num_cus/16 of
-            // them express workgroups (k_cg_fit's long-series path); fewer bulk blocks when the batch cannot
-            // fill them
-            const int cus = std::max(1, h->num_cus);
-            int xblocks = h->express_blocks >= 0 ? h->express_blocks : std::max(1, cus / 16);
-            if (xblocks >= cus) xblocks = cus - 1;
-            int blocks = h->grid_blocks_override;
-            if (blocks <= 0) blocks = std::max(1, cus - xblocks);
-            const int per_block = std::max(1, sts::cg_fit_series_per_block(p, q, I));
-            const int64_t need = (N + per_block - 1) / per_block;
-            if (blocks > need) blocks = (int)need;
-            if (xblocks > 0) {
-                RCCHK(h, h->xring.ensure(sts::kExpressRingBytes), "workspace");
-                RCCHK(h, h->xready.ensure(sts::kExpressReadyBytes), "workspace");
-                HIPCHK(h, hipMemsetAsync(h->xready.ptr, 0, sts::kExpressReadyBytes, s));
-            }
-            h->last_grid = blocks;
-            h->last_express = xblocks;
-            RCCHK(h, sts::launch_cg_fit(y, ldn, n, N, p, q, I, h->smear, init, init_status, d_coef, d_ll, d_status,
-                                        d_neval, d_ngrad, d_flags, h->ctl.as<unsigned long long>(), blocks, xblocks,
-                                        h->xring.as<unsigned char>(), h->xready.as<unsigned>(), s),
-                  "cg_fit");
-        }
-        HIPCHK(h, hipEventRecord(h->ev[3], s));
-    }
-    HIPCHK(h, hipMemcpyAsync(h->ctl_host, h->ctl.ptr, kCtlWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    int64_t grid = 0, xblocks = 0;
+    RCCHK(h, fit_kernels(h, h->ws, h->diff.as<double>(), ldn, n, N, p, q, I, method, d_user_init, d_coef, d_ll,
+                         d_status, d_neval, d_ngrad, d_flags, s, h->ev[2], &grid, &xblocks), "fit");
+    HIPCHK(h, hipEventRecord(h->ev[3], s));
+    h->last_grid = grid;
+    h->last_express = xblocks;
+    HIPCHK(h, hipMemcpyAsync(h->ctl_host, h->ws.ctl.ptr, kCtlWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    h->fit_ctl = true;
     HIPCHK(h, end_call(h, s));
     PendingStats &ps = h->pending;
     ps.N = N;
@@ -364,6 +430,8 @@ static void finish_stats(arima_handle *h) {
     st.express_f_passes = (int64_t)c[24];
     st.express_g_passes = (int64_t)c[25];
     st.express_blocks = ps.express;
+    st.fault = (int64_t)c[26];
+    for (int i = 0; i < 5; ++i) st.fault_info[i] = (int64_t)c[27 + i];
     // STS_TIMING builds: F-pass, G-pass, advance, select cycles (summed over waves), kernel span, drained time
     st.diag[0] = (int64_t)c[10];
     st.diag[1] = (int64_t)c[11];
@@ -372,10 +440,11 @@ static void finish_stats(arima_handle *h) {
     st.diag[4] = c[14] ? (int64_t)(c[14] - c[15]) : 0;
     st.diag[5] = (int64_t)c[16];
     st.grid_blocks = ps.grid;
-    // HR passes: 2 per column of each of the two least squares (+1 re-transform sweep over C rows)
+    // HR passes: 2 per column of each of the two least squares, minus the norm pass of an intercept column (the
+    // sum of ones needs no stream; arima_device.hpp ols_stage)
     const int M = std::max(p, q), m = M + 1;
-    if (ps.ar_only) st.hr_passes = N * (int64_t)(2 * (I + p));
-    else if (!ps.user_init) st.hr_passes = N * (int64_t)(2 * (1 + m) + 2 * k);
+    if (ps.ar_only) st.hr_passes = N * (int64_t)(2 * (I + p) - I);
+    else if (!ps.user_init) st.hr_passes = N * (int64_t)(2 * (1 + m) - 1 + 2 * k - I);
     // algorithmic flops: U*S*(2(p+q)+4) + G*S*(2(p+q)+4 + 2kq + 1+p+q + 2k) + W_HR
     const double S = std::max(n - M, 0);
     const double ff = 2.0 * (p + q) + 4, fg = ff + 2.0 * k * q + 1 + p + q + 2.0 * k;
@@ -443,7 +512,7 @@ int arima_fit_batch(arima_handle *h, const double *series, int64_t N, int32_t T,
     if (flags_out) HIPCHK(h, hipMemcpyAsync(flags_out, h->h_flags.ptr, (size_t)N, hipMemcpyDeviceToHost, s));
     HIPCHK(h, end_call(h, s));
     HIPCHK(h, hipStreamSynchronize(s));
-    return ARIMA_OK;
+    return check_fault(h);
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -647,36 +716,74 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
                                int32_t *d_order, double *d_coef, double *d_aic, int64_t *n_fits, hipStream_t s) {
     if (max_p < 0 || max_q < 0 || max_d < 0 || intercept_mode < 0 || intercept_mode > 2)
         return set_err(h, ARIMA_E_INVALID_ARG, "bad search bounds");
-    if (max_p > 5 || max_q > 5 || max_d > 16) return set_err(h, ARIMA_E_UNSUPPORTED, "p, q <= 5, d <= 16");
+    if (max_p > 5 || max_q > 5 || max_d > kMaxD) return set_err(h, ARIMA_E_UNSUPPORTED, "p, q <= 5, d <= 16");
     if (N < 0 || T < 0 || ld < T || !d_order || !d_coef || !d_aic) return set_err(h, ARIMA_E_INVALID_ARG, "bad shape");
+    h->pending = PendingStats{};
+    h->stats = arima_fit_stats{};
     if (N == 0) return ARIMA_OK;
     HIPCHK(h, hipSetDevice(h->device));
-    RCCHK(h, h->os_coef.ensure((size_t)N * 11 * sizeof(double)), "workspace");
-    RCCHK(h, h->os_ll.ensure((size_t)N * sizeof(double)), "workspace");
-    RCCHK(h, h->os_status.ensure((size_t)N * sizeof(int32_t)), "workspace");
-    RCCHK(h, h->os_neval.ensure((size_t)N * sizeof(int32_t)), "workspace");
-    RCCHK(h, h->os_ngrad.ensure((size_t)N * sizeof(int32_t)), "workspace");
-    RCCHK(h, h->os_flags.ensure((size_t)N), "workspace");
+    const int L = h->search_lanes;
+    for (int j = 0; j < L; ++j) {
+        SearchLane &ln = h->lanes[j];
+        if (!ln.stream) {
+            HIPCHK(h, hipStreamCreateWithFlags(&ln.stream, hipStreamNonBlocking));
+            HIPCHK(h, hipEventCreateWithFlags(&ln.ev_fit, hipEventDisableTiming));
+            HIPCHK(h, hipEventCreateWithFlags(&ln.ev_sel, hipEventDisableTiming));
+        }
+        RCCHK(h, ln.coef.ensure((size_t)N * 11 * sizeof(double)), "workspace");
+        RCCHK(h, ln.ll.ensure((size_t)N * sizeof(double)), "workspace");
+        RCCHK(h, ln.status.ensure((size_t)N * sizeof(int32_t)), "workspace");
+        RCCHK(h, ln.neval.ensure((size_t)N * sizeof(int32_t)), "workspace");
+        RCCHK(h, ln.ngrad.ensure((size_t)N * sizeof(int32_t)), "workspace");
+        RCCHK(h, ln.flags.ensure((size_t)N), "workspace");
+        // every workspace at its largest size before anything is enqueued: a growing DevBuf frees (hipFree
+        // synchronises the device) and would serialise the host loop below with the fits already in flight
+        RCCHK(h, ln.ws.init.ensure((size_t)N * 11 * sizeof(double)), "workspace");
+        RCCHK(h, ln.ws.hr_status.ensure((size_t)N * sizeof(int32_t)), "workspace");
+        RCCHK(h, ln.ws.ctl.ensure(kCtlWords * sizeof(unsigned long long)), "workspace");
+        RCCHK(h, ln.ws.xring.ensure(sts::kExpressRingBytes), "workspace");
+        RCCHK(h, ln.ws.xready.ensure(sts::kExpressReadyBytes), "workspace");
+    }
+    for (int d = 0; d <= max_d; ++d)
+        RCCHK(h, h->os_diff[d].ensure((size_t)N * round_up(std::max(T - d, 1), 16) * sizeof(double)), "workspace");
+    HIPCHK(h, hipEventRecord(h->ev[0], s));
     RCCHK(h, sts::launch_search_init(d_aic, d_order, d_coef, N, s), "search_init");
     const int i_lo = intercept_mode == 1 ? 1 : 0, i_hi = intercept_mode == 0 ? 0 : 1;
     int64_t fits = 0;
-    for (int d = 0; d <= max_d; ++d)
+    for (int d = 0; d <= max_d; ++d) {
+        // differencesOfOrderD once per d (ARIMA.scala:88), shared read-only by that d's fits on every lane
+        const int n = std::max(T - d, 0);
+        const int64_t ldn = round_up(std::max(n, 1), 16);
+        RCCHK(h, h->os_diff[d].ensure((size_t)N * ldn * sizeof(double)), "workspace");
+        if (!h->ev_diff[d]) HIPCHK(h, hipEventCreateWithFlags(&h->ev_diff[d], hipEventDisableTiming));
+        RCCHK(h, sts::launch_difference(d_series, ld, h->os_diff[d].as<double>(), ldn, N, T, d, 1, s), "difference");
+        HIPCHK(h, hipEventRecord(h->ev_diff[d], s));
         for (int p = 0; p <= max_p; ++p)
             for (int q = 0; q <= max_q; ++q)
                 for (int I = i_lo; I <= i_hi; ++I) {
                     // ARIMA(0,d,0) without intercept has no parameters: the reference throws (NoDataException);
-                    // fit_device_locked reports it per series and the select step skips it.
-                    int rc = fit_device_locked(h, d_series, N, T, ld, p, d, q, I, method, nullptr,
-                                               h->os_coef.as<double>(), h->os_ll.as<double>(),
-                                               h->os_status.as<int32_t>(), h->os_neval.as<int32_t>(),
-                                               h->os_ngrad.as<int32_t>(), h->os_flags.as<uint8_t>(), s);
-                    if (rc != ARIMA_OK) return rc;
-                    RCCHK(h, sts::launch_search_select(h->os_coef.as<double>(), h->os_ll.as<double>(),
-                                                       h->os_status.as<int32_t>(), h->os_flags.as<uint8_t>(), N, p,
-                                                       d, q, I, d_aic, d_order, d_coef, s),
+                    // fit_kernels reports it per series and the select step skips it.
+                    SearchLane &ln = h->lanes[fits % L];
+                    HIPCHK(h, hipStreamWaitEvent(ln.stream, h->ev_diff[d], 0));
+                    if (ln.sel_recorded) HIPCHK(h, hipStreamWaitEvent(ln.stream, ln.ev_sel, 0));  // outputs read
+                    int64_t grid = 0, xb = 0;
+                    RCCHK(h, fit_kernels(h, ln.ws, h->os_diff[d].as<double>(), ldn, n, N, p, q, I, method, nullptr,
+                                         ln.coef.as<double>(), ln.ll.as<double>(), ln.status.as<int32_t>(),
+                                         ln.neval.as<int32_t>(), ln.ngrad.as<int32_t>(), ln.flags.as<uint8_t>(),
+                                         ln.stream, nullptr, &grid, &xb, L > 1), "fit");
+                    HIPCHK(h, hipEventRecord(ln.ev_fit, ln.stream));
+                    // candidates are merged in grid order on the call's stream (first minimum wins, as minBy)
+                    HIPCHK(h, hipStreamWaitEvent(s, ln.ev_fit, 0));
+                    RCCHK(h, sts::launch_search_select(ln.coef.as<double>(), ln.ll.as<double>(),
+                                                       ln.status.as<int32_t>(), ln.flags.as<uint8_t>(), N, p, d, q, I,
+                                                       d_aic, d_order, d_coef, s),
                           "search_select");
+                    HIPCHK(h, hipEventRecord(ln.ev_sel, s));
+                    ln.sel_recorded = true;
                     ++fits;
                 }
+    }
+    HIPCHK(h, hipEventRecord(h->ev[3], s));
     if (n_fits) *n_fits = fits;
     return ARIMA_OK;
 }

@@ -61,11 +61,13 @@ class FitStats(ctypes.Structure):
                 ("spec_hits", ctypes.c_int64), ("wave_multi_passes", ctypes.c_int64), ("spec_chains", ctypes.c_int64),
                 ("express_blocks", ctypes.c_int64), ("express_series", ctypes.c_int64),
                 ("express_f_passes", ctypes.c_int64), ("express_g_passes", ctypes.c_int64),
+                ("fault", ctypes.c_int64), ("fault_info", ctypes.c_int64 * 5),
                 ("diag", ctypes.c_int64 * 6)]
 
     def as_dict(self):
         d = {name: getattr(self, name) for name, _ in self._fields_}
         d["diag"] = list(self.diag)
+        d["fault_info"] = list(self.fault_info)
         return d
 
 

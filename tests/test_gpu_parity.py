@@ -382,3 +382,40 @@ def test_long_fits_through_express(engine):
     st = engine.stats()
     check_fit(res, arr, "c4_515_T512")
     assert st["express_series"] > 0, st
+
+
+def test_express_ring_under_pressure_matches_bulk(engine):
+    # a small batch of mostly-MaxEval fits: every bulk wave drains early and turns express, so nearly every group of
+    # every wave holds a ticket while bulk waves still donate -- the hand-off ring's worst case (a fill must never
+    # overwrite an entry before its ticket holder has read it). Results must equal the express-free run bit for bit.
+    import torch
+    N, T = 1 << 16, 1024
+    s = _device_sample(engine, N, T, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 20261015)
+    outs = {}
+    for xb in (0, -1):
+        engine.set_option("express_blocks", xb)
+        try:
+            r = [torch.empty((N, 6), dtype=torch.float64, device=s.device),
+                 torch.empty(N, dtype=torch.float64, device=s.device)] + \
+                [torch.empty(N, dtype=torch.int32, device=s.device) for _ in range(3)] + \
+                [torch.empty(N, dtype=torch.uint8, device=s.device)]
+            engine.fit_batch_device(s.data_ptr(), N, T, T, 3, 1, 2, True, *[t.data_ptr() for t in r])
+            st = engine.stats()
+        finally:
+            engine.set_option("express_blocks", -1)
+        outs[xb] = ([t.cpu().numpy() for t in r], st)
+    (a, _), (b, st) = outs[0], outs[-1]
+    assert st["express_series"] > 1000, st
+    for x, y in zip(a, b):
+        assert _same(x, y)
+
+
+def test_order_search_T1024_matches_oracle(engine):
+    # C5 at its own length: the full (d <= 2, p <= 5, q <= 5, +-c) grid on 16 C2-shaped series of T = 1024, fits of
+    # consecutive grid points running concurrently on the search's lanes; order, coefficients and AIC bit-exact
+    s = _device_sample(engine, 16, 1024, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 4711).cpu().numpy()
+    order, coef, aic = engine.order_search(s, 5, 2, 5, 2)
+    eo, ec, ea = O.order_search(s, 5, 2, 5, 2)
+    assert np.array_equal(order, eo), (order, eo)
+    assert _same(coef, ec)
+    assert _same(aic, ea)

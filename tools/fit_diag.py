@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--order", default="2,1,2,1")
     ap.add_argument("--smear", type=int, default=1)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--express-blocks", type=int, default=-1)
     a = ap.parse_args()
     import torch
     import sparkts_amd._lib as L
@@ -25,6 +26,7 @@ def main():
             (5, 1, 5, 1): [0.1, 0.4, -0.2, 0.1, 0.05, -0.05, 0.3, 0.2, -0.1, 0.05, 0.05]}[(p, d, q, I)]
     eng = L.Engine.get(0)
     eng.set_option("smear", a.smear)
+    eng.set_option("express_blocks", a.express_blocks)
     N, T, k = a.series, a.T, p + q + I
     s = torch.empty((N, T), dtype=torch.float64, device="cuda")
     eng.sample_device(s.data_ptr(), N, T, T, p, d, q, I, base, 0.05 if k < 11 else 0.02, 20261015)
@@ -51,12 +53,29 @@ def main():
         fin = outs[1].cpu().numpy()
         path = outs[5].cpu().numpy()
         ne = nev.numpy()
-        t0 = fin.min()
+        ng = outs[4].cpu().numpy()
+        cf = outs[0].cpu().numpy()
+        ok = outs[2].cpu().numpy() >= 0
+        t_st, t_dn = cf[:, 0], cf[:, 1]
+        t0 = t_st.min()
         ms = (fin - t0) / 1e5
+        st_ms = (t_st - t0) / 1e5
+        dn_ms = np.where(t_dn > 0, (t_dn - t0) / 1e5, -1.0)
+
+        def rec(i):
+            return dict(n_eval=int(ne[i]), n_grad=int(ng[i]), start_ms=round(float(st_ms[i]), 2),
+                        donate_ms=round(float(dn_ms[i]), 2), finish_ms=round(float(ms[i]), 2), path=int(path[i]))
         order = np.argsort(-ne)[:20]
-        out["slowest_series"] = [dict(n_eval=int(ne[i]), finish_ms=float(ms[i]), path=int(path[i])) for i in order]
-        out["latest_finishers"] = [dict(n_eval=int(ne[i]), finish_ms=float(ms[i]), path=int(path[i]))
-                                   for i in np.argsort(-ms)[:20]]
+        out["slowest_series"] = [rec(i) for i in order]
+        out["latest_finishers"] = [rec(i) for i in np.argsort(-ms)[:20]]
+        top = np.argsort(-ne)[:max(1, N // 1000)]
+        dur = ms - st_ms
+        out["top_0p1pct"] = dict(count=int(len(top)), n_eval_min=int(ne[top].min()),
+                                 start_ms_q=[float(np.quantile(st_ms[top], x)) for x in (0.1, 0.5, 0.9)],
+                                 dur_ms_q=[float(np.quantile(dur[top], x)) for x in (0.1, 0.5, 0.9, 1.0)],
+                                 dur_per_eval_us=float(np.median(dur[top] / ne[top]) * 1e3),
+                                 express_frac=float((path[top] == 2).mean()))
+        out["duration_ms_quantiles"] = {str(qq): float(np.quantile(dur, qq)) for qq in (0.5, 0.9, 0.99, 0.999, 1.0)}
         out["finish_ms_quantiles"] = {str(qq): float(np.quantile(ms, qq)) for qq in (0.5, 0.9, 0.99, 0.999, 1.0)}
         out["express_count"] = int((path == 2).sum())
     out["n_eval_p999"] = float(nev.double().quantile(0.999)) if N <= 1 << 24 else None
