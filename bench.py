@@ -13,6 +13,10 @@ collective; gloo carries only the timing barrier and the max-over-ranks reductio
   --series S        series per GPU (weak scaling, default 1M: configs[1], and configs[2] read per GPU)
   --total-series S  fixed total over all GPUs (strong scaling: configs[2] = 8M series sharded over N GPUs)
   --smear 0|1       Breeze overlap reading at ARIMA.scala:526 (default 1)
+  --pipeline P      fit contexts in rotation (arima_set_option "fit_pipeline", default 2): step i+1's differencing,
+                    init and bulk fit run while step i's slowest series finish; every step is still a
+                    complete fit of every series, into its own output buffers (one set per context)
+  --e2e 0|1         also time one arima_fit_batch call from pageable host memory (default 1)
   --dry-run         no GPU: ranks compute their shards and report (tests/test_multirank.py)
 Prints ONE JSON line on rank 0.
 """
@@ -81,7 +85,8 @@ def cpu_baseline(series_host, p, d, q, I, smear, target_s):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     affinity = len(os.sched_getaffinity(0))
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or affinity
+    omp_env = os.environ.get("OMP_NUM_THREADS")
+    cores = int(omp_env or "0") or affinity
     cores = max(1, min(cores, affinity, 64))
     os.environ["OMP_NUM_THREADS"] = str(cores)
     O.lib()
@@ -100,8 +105,24 @@ def cpu_baseline(series_host, p, d, q, I, smear, target_s):
             "host_cpus": os.cpu_count(), "affinity_cpus": affinity,
             "sample": f"{len(sample)} synthetic series of the benchmark workload (first rows of rank 0's shard) "
                       f"fitted {rounds}x in {dt:.1f} s by the C restatement oracle/arima_oracle.c "
-                      f"(OpenMP, {cores} threads = this process's CPU affinity; the box reports "
-                      f"{os.cpu_count()} CPUs in all; {conv}/{len(sample)} converged); not the spark-ts JVM"}
+                      f"(OpenMP, {cores} threads: OMP_NUM_THREADS={omp_env}, the lease's CPU share; this process "
+                      f"may run on {affinity} CPUs and the box reports {os.cpu_count()} in all; "
+                      f"{conv}/{len(sample)} converged); not the spark-ts JVM"}
+
+
+def end_to_end(eng, series, p, d, q, I):
+    """the same fit from the caller's (pageable) host memory through the blocking host entry
+    point arima_fit_batch -- chunked uploads overlapped with the fits of earlier chunks, results back through pinned
+    staging into the caller's arrays. One warm-up call on the first chunk sizes the staging buffers."""
+    host = series.cpu().numpy()
+    eng.fit_batch(host[: 1 << 18], p, d, q, bool(I))
+    t0 = time.perf_counter()
+    r = eng.fit_batch(host, p, d, q, bool(I))
+    dt = time.perf_counter() - t0
+    return {"value": len(host) / dt, "unit": "series fitted/sec", "seconds": dt, "series": len(host),
+            "bytes_in": int(host.nbytes), "converged_fraction": float((r["status"] == 0).mean()),
+            "path": "arima_fit_batch: pageable host N x T -> HBM (chunks of 262144 over 3 fit contexts) -> "
+                    "difference/HR/CG fit -> pinned staging -> caller's arrays"}
 
 
 def main():
@@ -115,6 +136,8 @@ def main():
     ap.add_argument("--smear", type=int, default=1, choices=[0, 1])
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (0 = skip)")
     ap.add_argument("--grid-blocks", type=int, default=0)
+    ap.add_argument("--pipeline", type=int, default=2)
+    ap.add_argument("--e2e", type=int, default=1, choices=[0, 1])
     ap.add_argument("--dry-run", action="store_true")
     args = ap.parse_args()
 
@@ -172,28 +195,35 @@ def main():
     dev = torch.device("cuda", local)
     eng = L.Engine.get(local)
     eng.set_option("smear", args.smear)
+    eng.set_option("fit_pipeline", args.pipeline)
     if args.grid_blocks:
         eng.set_option("grid_blocks", args.grid_blocks)
 
     series = torch.empty((N, T), dtype=torch.float64, device=dev)
     eng.sample_device(series.data_ptr(), N, T, T, p, d, q, I, base, jitter, SEED, first)
-    coef = torch.empty((N, k), dtype=torch.float64, device=dev)
-    ll = torch.empty(N, dtype=torch.float64, device=dev)
-    status = torch.empty(N, dtype=torch.int32, device=dev)
-    n_eval = torch.empty(N, dtype=torch.int32, device=dev)
-    n_grad = torch.empty(N, dtype=torch.int32, device=dev)
-    flags = torch.empty(N, dtype=torch.uint8, device=dev)
+    # one output set per fit context: pipelined steps never write the same buffers concurrently
+    outs = [dict(coef=torch.empty((N, k), dtype=torch.float64, device=dev),
+                 ll=torch.empty(N, dtype=torch.float64, device=dev),
+                 status=torch.empty(N, dtype=torch.int32, device=dev),
+                 n_eval=torch.empty(N, dtype=torch.int32, device=dev),
+                 n_grad=torch.empty(N, dtype=torch.int32, device=dev),
+                 flags=torch.empty(N, dtype=torch.uint8, device=dev)) for _ in range(max(1, args.pipeline))]
     torch.cuda.synchronize(dev)
+    calls = [0]
 
     def step():
-        # asynchronous: enqueues difference -> HR init -> CG fit on the handle's stream and returns
-        eng.fit_batch_device(series.data_ptr(), N, T, T, p, d, q, I, coef.data_ptr(), ll.data_ptr(),
-                             status.data_ptr(), n_eval.data_ptr(), n_grad.data_ptr(), flags.data_ptr(), blocking=False)
+        # asynchronous: enqueues difference -> HR init -> CG fit on the next fit context's stream and returns
+        o = outs[calls[0] % len(outs)]
+        calls[0] += 1
+        eng.fit_batch_device(series.data_ptr(), N, T, T, p, d, q, I, o["coef"].data_ptr(), o["ll"].data_ptr(),
+                             o["status"].data_ptr(), o["n_eval"].data_ptr(), o["n_grad"].data_ptr(),
+                             o["flags"].data_ptr(), blocking=False)
 
     for i in range(args.warmup):
         t0 = time.perf_counter()
         step()
-        s = eng.stats()                   # waits for the step's device work
+        eng.synchronize()
+        s = eng.stats()
         log(f"[rank {rank}] warmup {i}: {time.perf_counter() - t0:.3f} s (cg {s['ms_cg_fit']:.1f} ms)")
     barrier()
     eng.synchronize()
@@ -209,7 +239,7 @@ def main():
     log(f"[rank {rank}] {args.steps} steps in {elapsed:.3f} s; last step: difference {s0['ms_difference']:.1f} ms, "
         f"hr {s0['ms_hr_init']:.1f} ms, cg {s0['ms_cg_fit']:.1f} ms")
 
-    st_h = status.cpu().numpy()
+    st_h = outs[(calls[0] - 1) % len(outs)]["status"].cpu().numpy()
     conv = float((st_h == 0).mean()) if N else 1.0
     n = T - d
     M = max(p, q)
@@ -271,6 +301,8 @@ def main():
                                          "multi": s0["wave_multi_passes"]}},
             "cpu_baseline": None,
         }
+        if world == 1 and args.e2e:
+            result["end_to_end_host"] = end_to_end(eng, series, p, d, q, I)
         if world == 1 and args.cpu_seconds > 0:
             host = series[: 4096].cpu().numpy()
             result["cpu_baseline"] = cpu_baseline(host, p, d, q, I, args.smear, args.cpu_seconds)

@@ -15,8 +15,13 @@
  *     pointer after return. `*_device` entry points take device (HBM) pointers and a hipStream_t passed as
  *     `void*` (NULL = the handle's own stream) and are asynchronous w.r.t. the host: they enqueue their work
  *     and return (results are valid once that stream reaches the call's end). Calls on one handle are also
- *     ordered on the device whichever streams they use, because they share the handle's workspaces.
- *     arima_get_last_stats waits for the last call's device work. Host-buffer entry points block.
+ *     ordered on the device whichever streams they use, because they share the handle's workspaces --
+ *     except fit calls under the "fit_pipeline" option (arima_set_option): with fit_pipeline = P > 1,
+ *     consecutive arima_fit_batch_device calls rotate over P fit contexts and may run concurrently (the
+ *     caller must not feed one fit's outputs to a later fit before arima_synchronize). Every non-fit call
+ *     still waits for all earlier calls. arima_get_last_stats waits for the last call's device work.
+ *     Host-buffer entry points block (arima_fit_batch pipelines its own chunks internally: "host_chunk",
+ *     "host_pipeline").
  *   - A batch is N series of equal length T, series-major: element t of series i is series[i*ld + t]
  *     (ld == T for the host-buffer entry points). One call = one Spark partition bucketed by length.
  *   - Coefficient layout per series is the reference's: [c?, phi_1..phi_p, theta_1..theta_q]
@@ -104,7 +109,10 @@ int         arima_num_params(int p, int q, int include_intercept);
 int         arima_get_last_stats(const arima_handle *h, arima_fit_stats *out);
 /* Blocks until the device work of every call issued on the handle so far has finished. */
 int         arima_synchronize(arima_handle *h);
-/* Tuning knob for the in-kernel scheduler (0 = default). Not part of the reference contract. */
+/* Tuning knobs (not part of the reference contract): "smear" (Breeze reading at ARIMA.scala:526, default 1),
+ * "fit_pipeline" (fit contexts in rotation for *_device fits, 1..4, default 1), "host_chunk" / "host_pipeline"
+ * (series per chunk and contexts of the chunked host path, default 262144 / 3), "express_blocks",
+ * "grid_blocks", "search_lanes" (in-kernel scheduler and order-search concurrency). */
 int         arima_set_option(arima_handle *h, const char *name, int64_t value);
 
 /* ---- ARIMA.fitModel over a batch (ARIMA.scala:79-116) ----------------------------------------------- *

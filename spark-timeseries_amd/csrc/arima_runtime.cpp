@@ -77,6 +77,28 @@ struct SearchLane {
 
 constexpr int kMaxSearchLanes = 8;
 constexpr int kMaxD = 16;
+constexpr int kMaxPipeline = 4;
+
+// One fit context: what a fit call needs for itself (stream, differenced-series workspace, HR init, kernel counters,
+// timing events, pinned counter copy, host-path staging). Fit calls rotate over h->pipeline contexts, so with
+// pipeline > 1 consecutive fits run concurrently and the tail of one fit kernel (its slowest series) overlaps the
+// next fit's differencing, init and bulk work; a context is reused only after its previous call has finished.
+struct FitCtx {
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[kNumEvents] = {};
+    hipEvent_t ev_done = nullptr;             // end of this context's last call
+    bool has_done = false;
+    DevBuf diff;
+    FitWs ws;
+    unsigned long long *ctl_host = nullptr;   // pinned
+    PendingStats pending;
+    bool fit_ctl = false;                     // ctl_host holds (or will hold, in stream order) the kernel counters
+    // host path (arima_fit_batch): device copies of one chunk and pinned staging of its input and outputs
+    DevBuf d_series, d_coef, d_ll, d_status, d_neval, d_ngrad, d_flags, d_uinit;
+    void *pin = nullptr;
+    size_t pin_bytes = 0;
+    int64_t chunk_first = -1, chunk_n = 0;    // the chunk whose results wait in `pin`
+};
 
 }  // namespace
 
@@ -85,22 +107,26 @@ struct arima_handle {
     int num_cus = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[kNumEvents] = {};
-    hipEvent_t ev_done = nullptr;     // end of the last call's device work (serialises workspace reuse across streams)
+    hipEvent_t ev_done = nullptr;     // end of the last non-fit call's device work
     bool has_done = false;
     mutable std::mutex mu;
     std::string err;
     arima_fit_stats stats{};
-    PendingStats pending;
-    bool fit_ctl = false;          // ctl_host holds (or will hold, in stream order) the last fit's kernel counters
-    int smear = 1;            // Breeze 0.12 overlap semantics at ARIMA.scala:526: element-wise copy
+    int smear = 1;           // Breeze 0.12 overlap semantics at ARIMA.scala:526: element-wise copy
     int grid_blocks_override = 0;
     int express_blocks = -1;       // k_cg_fit express workgroups (-1: num_cus / 16)
     int64_t last_express = 0;
     int64_t last_grid = 0;
     int search_lanes = 4;          // concurrent fits of the order search
-    // device workspaces
+    int pipeline = 1;              // fit contexts in rotation (option "fit_pipeline")
+    int host_pipeline = 3;         // contexts the chunked host path rotates over
+    int64_t host_chunk = 1 << 18;  // series per chunk of the host path (option "host_chunk")
+    unsigned fit_seq = 0;          // fit calls so far (selects the context)
+    int stats_ctx = -1;            // context of the last fit (arima_get_last_stats), -1: none
+    arima_fit_stats host_acc{};    // host path: counters summed over its chunks
+    FitCtx fctx[kMaxPipeline];
+    // device workspaces of the building blocks
     DevBuf diff;
-    FitWs ws;
     // host-API staging
     DevBuf h_series, h_coef, h_ll, h_status, h_neval, h_ngrad, h_flags, h_uinit, h_aux;
     // order search: the differenced series per d, the concurrent fit lanes, host-API staging of the orders
@@ -108,7 +134,6 @@ struct arima_handle {
     hipEvent_t ev_diff[kMaxD + 1] = {};
     SearchLane lanes[kMaxSearchLanes];
     DevBuf os_order;
-    unsigned long long *ctl_host = nullptr;   // pinned
 };
 
 namespace {
@@ -197,8 +222,14 @@ int arima_create(int device, arima_handle **out) {
     for (auto &e : h->ev)
         if (rc == ARIMA_OK && hipEventCreate(&e) != hipSuccess) rc = ARIMA_E_DEVICE;
     if (rc == ARIMA_OK && hipEventCreateWithFlags(&h->ev_done, hipEventDisableTiming) != hipSuccess) rc = ARIMA_E_DEVICE;
-    if (rc == ARIMA_OK && hipHostMalloc((void **)&h->ctl_host, kCtlWords * sizeof(unsigned long long), 0) != hipSuccess)
-        rc = ARIMA_E_OOM;
+    for (auto &c : h->fctx) {
+        if (rc == ARIMA_OK && hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking) != hipSuccess) rc = ARIMA_E_DEVICE;
+        for (auto &e : c.ev)
+            if (rc == ARIMA_OK && hipEventCreate(&e) != hipSuccess) rc = ARIMA_E_DEVICE;
+        if (rc == ARIMA_OK && hipEventCreateWithFlags(&c.ev_done, hipEventDisableTiming) != hipSuccess) rc = ARIMA_E_DEVICE;
+        if (rc == ARIMA_OK && hipHostMalloc((void **)&c.ctl_host, kCtlWords * sizeof(unsigned long long), 0) != hipSuccess)
+            rc = ARIMA_E_OOM;
+    }
     if (rc != ARIMA_OK) {
         arima_destroy(h);
         return rc;
@@ -220,12 +251,22 @@ int arima_destroy(arima_handle *h) {
         if (l.ev_fit) hipEventDestroy(l.ev_fit);
         if (l.ev_sel) hipEventDestroy(l.ev_sel);
     }
+    for (auto &c : h->fctx) {
+        if (c.stream) {
+            hipStreamSynchronize(c.stream);
+            hipStreamDestroy(c.stream);
+        }
+        for (auto &e : c.ev)
+            if (e) hipEventDestroy(e);
+        if (c.ev_done) hipEventDestroy(c.ev_done);
+        if (c.ctl_host) hipHostFree(c.ctl_host);
+        if (c.pin) hipHostFree(c.pin);
+    }
     for (auto &e : h->ev_diff)
         if (e) hipEventDestroy(e);
     for (auto &e : h->ev)
         if (e) hipEventDestroy(e);
     if (h->ev_done) hipEventDestroy(h->ev_done);
-    if (h->ctl_host) hipHostFree(h->ctl_host);
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;                                  // every DevBuf workspace frees itself
     return ARIMA_OK;
@@ -233,28 +274,29 @@ int arima_destroy(arima_handle *h) {
 
 const char *arima_last_error(const arima_handle *h) { return h ? h->err.c_str() : "null handle"; }
 
-static void finish_stats(arima_handle *h);
+static void finish_stats(arima_handle *h, FitCtx &c);
 
 int arima_get_last_stats(const arima_handle *hc, arima_fit_stats *out) {
     if (!hc || !out) return ARIMA_E_INVALID_ARG;
     arima_handle *h = const_cast<arima_handle *>(hc);   // the lazy completion below only fills h->stats
     std::lock_guard<std::mutex> lk(h->mu);
-    if (h->pending.valid) {
+    if (h->stats_ctx >= 0 && h->fctx[h->stats_ctx].pending.valid) {
+        FitCtx &c = h->fctx[h->stats_ctx];
         hipSetDevice(h->device);
-        if (hipEventSynchronize(h->ev_done) != hipSuccess) return set_err(h, ARIMA_E_DEVICE, "stats: device error");
-        finish_stats(h);
+        if (hipEventSynchronize(c.ev_done) != hipSuccess) return set_err(h, ARIMA_E_DEVICE, "stats: device error");
+        finish_stats(h, c);
     }
     *out = h->stats;
     return ARIMA_OK;
 }
 
-// The last fit's kernel recorded a watchdog fault (k_cg_fit's hand-off): its results are incomplete.
-static int check_fault(arima_handle *h) {
-    if (h->fit_ctl && h->ctl_host[26] != 0) {
-        h->fit_ctl = false;                      // reported once
+// A finished fit kernel of context c recorded a watchdog fault (k_cg_fit's hand-off): its results are incomplete.
+static int check_fault(arima_handle *h, FitCtx &c) {
+    if (c.fit_ctl && c.ctl_host[26] != 0) {
+        c.fit_ctl = false;                      // reported once
         char msg[160];
-        snprintf(msg, sizeof msg, "fit kernel watchdog fault %llu (info %llu %llu %llu %llu %llu)", h->ctl_host[26],
-                 h->ctl_host[27], h->ctl_host[28], h->ctl_host[29], h->ctl_host[30], h->ctl_host[31]);
+        snprintf(msg, sizeof msg, "fit kernel watchdog fault %llu (info %llu %llu %llu %llu %llu)", c.ctl_host[26],
+                 c.ctl_host[27], c.ctl_host[28], c.ctl_host[29], c.ctl_host[30], c.ctl_host[31]);
         return set_err(h, ARIMA_E_DEVICE, msg);
     }
     return ARIMA_OK;
@@ -265,7 +307,12 @@ int arima_synchronize(arima_handle *h) {
     std::lock_guard<std::mutex> lk(h->mu);
     HIPCHK(h, hipSetDevice(h->device));
     if (h->has_done) HIPCHK(h, hipEventSynchronize(h->ev_done));
-    return check_fault(h);
+    int rc = ARIMA_OK;
+    for (auto &c : h->fctx) {
+        if (c.has_done) HIPCHK(h, hipEventSynchronize(c.ev_done));
+        if (rc == ARIMA_OK) rc = check_fault(h, c);
+    }
+    return rc;
 }
 
 int arima_set_option(arima_handle *h, const char *name, int64_t value) {
@@ -278,19 +325,43 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
         h->search_lanes = (int)std::min<int64_t>(kMaxSearchLanes, std::max<int64_t>(1, value));
         return ARIMA_OK;
     }
+    if (!strcmp(name, "fit_pipeline")) {
+        h->pipeline = (int)std::min<int64_t>(kMaxPipeline, std::max<int64_t>(1, value));
+        return ARIMA_OK;
+    }
+    if (!strcmp(name, "host_pipeline")) {
+        h->host_pipeline = (int)std::min<int64_t>(kMaxPipeline, std::max<int64_t>(1, value));
+        return ARIMA_OK;
+    }
+    if (!strcmp(name, "host_chunk")) { h->host_chunk = std::max<int64_t>(1, value); return ARIMA_OK; }
     return set_err(h, ARIMA_E_INVALID_ARG, "unknown option");
 }
 
 // ---------------------------------------------------------------------------------------------------------
-// Every device call waits (on the device, not the host) for the previous call's work: the handle's workspaces are
-// shared by all calls, whichever stream they are issued on.
+// Ordering. A non-fit call waits (on the device, not the host) for every earlier call: the building blocks share
+// the handle's workspaces, and any call may read an earlier call's outputs. A fit call waits for the earlier
+// non-fit calls (e.g. the sampler that wrote its input) and for the previous call on its own context; with
+// fit_pipeline = 1 (the default) that is the previous fit, so calls run in issue order.
 static void begin_call(arima_handle *h, hipStream_t s) {
     if (h->has_done) hipStreamWaitEvent(s, h->ev_done, 0);
+    for (auto &c : h->fctx)
+        if (c.has_done) hipStreamWaitEvent(s, c.ev_done, 0);
 }
 
 static hipError_t end_call(arima_handle *h, hipStream_t s) {
     hipError_t e = hipEventRecord(h->ev_done, s);
     if (e == hipSuccess) h->has_done = true;
+    return e;
+}
+
+static void begin_fit(arima_handle *h, FitCtx &c, hipStream_t s) {
+    if (h->has_done) hipStreamWaitEvent(s, h->ev_done, 0);
+    if (c.has_done) hipStreamWaitEvent(s, c.ev_done, 0);
+}
+
+static hipError_t end_fit(FitCtx &c, hipStream_t s) {
+    hipError_t e = hipEventRecord(c.ev_done, s);
+    if (e == hipSuccess) c.has_done = true;
     return e;
 }
 
@@ -357,10 +428,28 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
     return ARIMA_OK;
 }
 
-static int fit_device_locked(arima_handle *h, const double *d_series, int64_t N, int32_t T, int64_t ld, int32_t p,
-                             int32_t d, int32_t q, int32_t I, int32_t method, const double *d_user_init,
-                             double *d_coef, double *d_ll, int32_t *d_status, int32_t *d_neval, int32_t *d_ngrad,
-                             uint8_t *d_flags, hipStream_t s) {
+// Grow the workspaces of the first `count` contexts to an N x ldn batch with k parameters at once, so that no
+// workspace grows (hipFree synchronises the device) while fits of other contexts are in flight.
+static int reserve_fit_ws(arima_handle *h, int count, int64_t N, int64_t ldn, int k) {
+    for (int j = 0; j < count; ++j) {
+        FitCtx &c = h->fctx[j];
+        RCCHK(h, c.diff.ensure((size_t)N * ldn * sizeof(double)), "workspace");
+        RCCHK(h, c.ws.init.ensure((size_t)N * std::max(k, 1) * sizeof(double)), "workspace");
+        RCCHK(h, c.ws.hr_status.ensure((size_t)N * sizeof(int32_t)), "workspace");
+        RCCHK(h, c.ws.ctl.ensure(kCtlWords * sizeof(unsigned long long)), "workspace");
+        RCCHK(h, c.ws.xring.ensure(sts::kExpressRingBytes), "workspace");
+        RCCHK(h, c.ws.xready.ensure(sts::kExpressReadyBytes), "workspace");
+    }
+    return ARIMA_OK;
+}
+
+// One fit on context c, enqueued on stream s (the caller has ordered s after what the fit depends on).
+// shared_gpu: fits of other contexts may run concurrently, so the fit kernel's drained workgroups exit (making room
+// for the next fit) instead of joining its express pool.
+static int fit_device_locked(arima_handle *h, FitCtx &c, int ci, int reserve, const double *d_series, int64_t N,
+                             int32_t T, int64_t ld, int32_t p, int32_t d, int32_t q, int32_t I, int32_t method,
+                             const double *d_user_init, double *d_coef, double *d_ll, int32_t *d_status,
+                             int32_t *d_neval, int32_t *d_ngrad, uint8_t *d_flags, hipStream_t s, bool shared_gpu) {
     RCCHK(h, check_orders(h, p, d, q, I), "orders");
     if (N < 0 || T < 0 || ld < T) return set_err(h, ARIMA_E_INVALID_ARG, "bad shape");
     if (!d_coef || !d_ll || !d_status) return set_err(h, ARIMA_E_INVALID_ARG, "null output");
@@ -368,25 +457,24 @@ static int fit_device_locked(arima_handle *h, const double *d_series, int64_t N,
     const int k = I + p + q;
     const int n = std::max(T - d, 0);
     const int64_t ldn = round_up(std::max(n, 1), 16);
-    h->pending = PendingStats{};
+    c.pending = PendingStats{};
     h->stats = arima_fit_stats{};
+    h->stats_ctx = ci;
     if (N == 0) return ARIMA_OK;
-    begin_call(h, s);
 
-    RCCHK(h, h->diff.ensure((size_t)N * ldn * sizeof(double)), "workspace");
-    HIPCHK(h, hipEventRecord(h->ev[0], s));
-    RCCHK(h, sts::launch_difference(d_series, ld, h->diff.as<double>(), ldn, N, T, d, 1, s), "difference");
-    HIPCHK(h, hipEventRecord(h->ev[1], s));
+    RCCHK(h, reserve_fit_ws(h, reserve, N, ldn, k), "workspace");
+    HIPCHK(h, hipEventRecord(c.ev[0], s));
+    RCCHK(h, sts::launch_difference(d_series, ld, c.diff.as<double>(), ldn, N, T, d, 1, s), "difference");
+    HIPCHK(h, hipEventRecord(c.ev[1], s));
     int64_t grid = 0, xblocks = 0;
-    RCCHK(h, fit_kernels(h, h->ws, h->diff.as<double>(), ldn, n, N, p, q, I, method, d_user_init, d_coef, d_ll,
-                         d_status, d_neval, d_ngrad, d_flags, s, h->ev[2], &grid, &xblocks), "fit");
-    HIPCHK(h, hipEventRecord(h->ev[3], s));
+    RCCHK(h, fit_kernels(h, c.ws, c.diff.as<double>(), ldn, n, N, p, q, I, method, d_user_init, d_coef, d_ll,
+                         d_status, d_neval, d_ngrad, d_flags, s, c.ev[2], &grid, &xblocks, shared_gpu), "fit");
+    HIPCHK(h, hipEventRecord(c.ev[3], s));
     h->last_grid = grid;
     h->last_express = xblocks;
-    HIPCHK(h, hipMemcpyAsync(h->ctl_host, h->ws.ctl.ptr, kCtlWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-    h->fit_ctl = true;
-    HIPCHK(h, end_call(h, s));
-    PendingStats &ps = h->pending;
+    HIPCHK(h, hipMemcpyAsync(c.ctl_host, c.ws.ctl.ptr, kCtlWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    c.fit_ctl = true;
+    PendingStats &ps = c.pending;
     ps.N = N;
     ps.n = n;
     ps.p = p;
@@ -395,50 +483,50 @@ static int fit_device_locked(arima_handle *h, const double *d_series, int64_t N,
     ps.ar_only = p > 0 && q == 0;
     ps.user_init = d_user_init != nullptr;
     ps.cg = !ps.ar_only && method == ARIMA_METHOD_CSS_CGD && k > 0;
-    ps.grid = h->last_grid;
-    ps.express = h->last_express;
+    ps.grid = grid;
+    ps.express = xblocks;
     ps.valid = true;
     return ARIMA_OK;
 }
 
-// Completes the stats of the last fit once its device work has finished (arima_get_last_stats).
-static void finish_stats(arima_handle *h) {
-    const PendingStats &ps = h->pending;
+// Completes the stats of context c's last fit once its device work has finished.
+static void finish_stats(arima_handle *h, FitCtx &c) {
+    const PendingStats &ps = c.pending;
     arima_fit_stats st{};
     const int64_t N = ps.N;
     const int n = ps.n, p = ps.p, q = ps.q, I = ps.I, k = I + p + q;
     float ms = 0;
-    hipEventElapsedTime(&ms, h->ev[0], h->ev[1]);
+    hipEventElapsedTime(&ms, c.ev[0], c.ev[1]);
     st.ms_difference = ms;
-    hipEventElapsedTime(&ms, h->ev[1], h->ev[2]);
+    hipEventElapsedTime(&ms, c.ev[1], c.ev[2]);
     st.ms_hr_init = ms;
-    hipEventElapsedTime(&ms, h->ev[2], h->ev[3]);
+    hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
     st.ms_cg_fit = ms;
-    hipEventElapsedTime(&ms, h->ev[0], h->ev[3]);
+    hipEventElapsedTime(&ms, c.ev[0], c.ev[3]);
     st.ms_total = ms;
-    const unsigned long long *c = h->ctl_host;
-    st.f_passes = (int64_t)c[1];
-    st.g_passes = (int64_t)c[2];
-    st.n_eval = (int64_t)c[5];
-    st.n_grad = (int64_t)c[6];
-    st.wave_f_passes = (int64_t)c[3];
-    st.wave_g_passes = (int64_t)c[4];
-    st.spec_hits = (int64_t)c[7];
-    st.wave_multi_passes = (int64_t)c[8];
-    st.spec_chains = (int64_t)c[9];
-    st.express_series = (int64_t)c[23];
-    st.express_f_passes = (int64_t)c[24];
-    st.express_g_passes = (int64_t)c[25];
+    const unsigned long long *cc = c.ctl_host;
+    st.f_passes = (int64_t)cc[1];
+    st.g_passes = (int64_t)cc[2];
+    st.n_eval = (int64_t)cc[5];
+    st.n_grad = (int64_t)cc[6];
+    st.wave_f_passes = (int64_t)cc[3];
+    st.wave_g_passes = (int64_t)cc[4];
+    st.spec_hits = (int64_t)cc[7];
+    st.wave_multi_passes = (int64_t)cc[8];
+    st.spec_chains = (int64_t)cc[9];
+    st.express_series = (int64_t)cc[23];
+    st.express_f_passes = (int64_t)cc[24];
+    st.express_g_passes = (int64_t)cc[25];
     st.express_blocks = ps.express;
-    st.fault = (int64_t)c[26];
-    for (int i = 0; i < 5; ++i) st.fault_info[i] = (int64_t)c[27 + i];
+    st.fault = (int64_t)cc[26];
+    for (int i = 0; i < 5; ++i) st.fault_info[i] = (int64_t)cc[27 + i];
     // STS_TIMING builds: F-pass, G-pass, advance, select cycles (summed over waves), kernel span, drained time
-    st.diag[0] = (int64_t)c[10];
-    st.diag[1] = (int64_t)c[11];
-    st.diag[2] = (int64_t)c[12];
-    st.diag[3] = (int64_t)c[13];
-    st.diag[4] = c[14] ? (int64_t)(c[14] - c[15]) : 0;
-    st.diag[5] = (int64_t)c[16];
+    st.diag[0] = (int64_t)cc[10];
+    st.diag[1] = (int64_t)cc[11];
+    st.diag[2] = (int64_t)cc[12];
+    st.diag[3] = (int64_t)cc[13];
+    st.diag[4] = cc[14] ? (int64_t)(cc[14] - cc[15]) : 0;
+    st.diag[5] = (int64_t)cc[16];
     st.grid_blocks = ps.grid;
     // HR passes: 2 per column of each of the two least squares, minus the norm pass of an intercept column (the
     // sum of ones needs no stream; arima_device.hpp ols_stage)
@@ -453,7 +541,7 @@ static void finish_stats(arima_handle *h) {
     st.flops = (double)st.f_passes * S * ff + (double)st.g_passes * S * fg + (ps.user_init ? 0.0 : whr);
     st.n_series = N;
     h->stats = st;
-    h->pending.valid = false;
+    c.pending.valid = false;
 }
 
 int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_series, int32_t T, int64_t ld,
@@ -463,10 +551,93 @@ int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_se
                            uint8_t *d_flags_out, void *stream) {
     if (!h) return ARIMA_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
-    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
-    begin_call(h, s);
-    return fit_device_locked(h, d_series, n_series, T, ld, p, d, q, include_intercept, method, d_user_init,
-                             d_coef_out, d_css_ll_out, d_status_out, d_n_eval_out, d_n_grad_out, d_flags_out, s);
+    const int P = h->pipeline;
+    const int ci = (int)(h->fit_seq++ % (unsigned)P);
+    FitCtx &c = h->fctx[ci];
+    hipStream_t s = stream ? (hipStream_t)stream : c.stream;
+    HIPCHK(h, hipSetDevice(h->device));
+    begin_fit(h, c, s);
+    const int rc = fit_device_locked(h, c, ci, P, d_series, n_series, T, ld, p, d, q, include_intercept, method,
+                                     d_user_init, d_coef_out, d_css_ll_out, d_status_out, d_n_eval_out, d_n_grad_out,
+                                     d_flags_out, s, P > 1);
+    HIPCHK(h, end_fit(c, s));
+    return rc;
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// Host path (end to end from host memory). The batch is cut into chunks of h->host_chunk
+// series that rotate over h->host_pipeline contexts: chunk j's upload (from the caller's pageable buffer, staged by
+// the HIP runtime) runs while the fits of chunks j-1, j-2 are still on the device, so PCIe and compute overlap and
+// the tail of one chunk's fit kernel overlaps the next chunk's work. Results come back through pinned staging and
+// are copied to the caller's arrays when the context is reused (or at the end).
+// ---------------------------------------------------------------------------------------------------------
+namespace {
+struct HostOut {
+    double *coef, *ll;
+    int32_t *status, *n_eval, *n_grad;
+    uint8_t *flags;
+};
+
+// bytes of one chunk's results in pinned staging: coef (n*k), ll, status, n_eval, n_grad, flags
+inline size_t pin_layout(int64_t n, int k, size_t off[6]) {
+    size_t o = 0;
+    off[0] = o; o += round_up((int64_t)n * std::max(k, 1) * 8, 256);
+    off[1] = o; o += round_up(n * 8, 256);
+    off[2] = o; o += round_up(n * 4, 256);
+    off[3] = o; o += round_up(n * 4, 256);
+    off[4] = o; o += round_up(n * 4, 256);
+    off[5] = o; o += round_up(n, 256);
+    return o;
+}
+}  // namespace
+
+static void acc_stats(arima_fit_stats &a, const arima_fit_stats &s) {
+    a.ms_difference += s.ms_difference;
+    a.ms_hr_init += s.ms_hr_init;
+    a.ms_cg_fit += s.ms_cg_fit;
+    a.ms_total += s.ms_total;
+    a.f_passes += s.f_passes;
+    a.g_passes += s.g_passes;
+    a.hr_passes += s.hr_passes;
+    a.n_eval += s.n_eval;
+    a.n_grad += s.n_grad;
+    a.flops += s.flops;
+    a.n_series += s.n_series;
+    a.wave_f_passes += s.wave_f_passes;
+    a.wave_g_passes += s.wave_g_passes;
+    a.wave_multi_passes += s.wave_multi_passes;
+    a.spec_hits += s.spec_hits;
+    a.spec_chains += s.spec_chains;
+    a.express_series += s.express_series;
+    a.express_f_passes += s.express_f_passes;
+    a.express_g_passes += s.express_g_passes;
+    a.grid_blocks = s.grid_blocks;
+    a.express_blocks = s.express_blocks;
+    if (!a.fault && s.fault) {
+        a.fault = s.fault;
+        for (int i = 0; i < 5; ++i) a.fault_info[i] = s.fault_info[i];
+    }
+}
+
+// Wait for context c's chunk, copy its results to the caller's arrays and add its counters to h->host_acc.
+static int drain_chunk(arima_handle *h, FitCtx &c, int k, const HostOut &o) {
+    if (c.chunk_n <= 0) return ARIMA_OK;
+    HIPCHK(h, hipEventSynchronize(c.ev_done));
+    const int64_t f = c.chunk_first, n = c.chunk_n;
+    c.chunk_n = 0;
+    if (c.pending.valid) finish_stats(h, c);
+    acc_stats(h->host_acc, h->stats);
+    RCCHK(h, check_fault(h, c), "fault");
+    size_t off[6];
+    pin_layout(n, k, off);
+    const char *b = static_cast<const char *>(c.pin);
+    if (k > 0) memcpy(o.coef + f * k, b + off[0], (size_t)n * k * 8);
+    memcpy(o.ll + f, b + off[1], (size_t)n * 8);
+    memcpy(o.status + f, b + off[2], (size_t)n * 4);
+    if (o.n_eval) memcpy(o.n_eval + f, b + off[3], (size_t)n * 4);
+    if (o.n_grad) memcpy(o.n_grad + f, b + off[4], (size_t)n * 4);
+    if (o.flags) memcpy(o.flags + f, b + off[5], (size_t)n);
+    return ARIMA_OK;
 }
 
 int arima_fit_batch(arima_handle *h, const double *series, int64_t N, int32_t T, int32_t p, int32_t d, int32_t q,
@@ -477,42 +648,85 @@ int arima_fit_batch(arima_handle *h, const double *series, int64_t N, int32_t T,
     RCCHK(h, check_orders(h, p, d, q, I), "orders");
     if (N < 0 || T < 0 || (N > 0 && (!series || !coef_out || !css_ll_out || !status_out)))
         return set_err(h, ARIMA_E_INVALID_ARG, "bad arguments");
+    h->stats = arima_fit_stats{};
+    h->stats_ctx = -1;
     if (N == 0) return ARIMA_OK;
     HIPCHK(h, hipSetDevice(h->device));
     const int k = I + p + q;
-    const size_t kk = (size_t)std::max(k, 1);
-    hipStream_t s = h->stream;
-    begin_call(h, s);
-    RCCHK(h, h->h_series.ensure((size_t)N * std::max(T, 1) * sizeof(double)), "staging");
-    RCCHK(h, h->h_coef.ensure((size_t)N * kk * sizeof(double)), "staging");
-    RCCHK(h, h->h_ll.ensure((size_t)N * sizeof(double)), "staging");
-    RCCHK(h, h->h_status.ensure((size_t)N * sizeof(int32_t)), "staging");
-    RCCHK(h, h->h_neval.ensure((size_t)N * sizeof(int32_t)), "staging");
-    RCCHK(h, h->h_ngrad.ensure((size_t)N * sizeof(int32_t)), "staging");
-    RCCHK(h, h->h_flags.ensure((size_t)N), "staging");
-    if (T > 0) HIPCHK(h, hipMemcpyAsync(h->h_series.ptr, series, (size_t)N * T * sizeof(double), hipMemcpyHostToDevice, s));
-    const double *d_ui = nullptr;
-    if (user_init && k > 0) {
-        RCCHK(h, h->h_uinit.ensure((size_t)N * k * sizeof(double)), "staging");
-        HIPCHK(h, hipMemcpyAsync(h->h_uinit.ptr, user_init, (size_t)N * k * sizeof(double), hipMemcpyHostToDevice, s));
-        d_ui = h->h_uinit.as<double>();
-    } else if (user_init) {
-        RCCHK(h, h->h_uinit.ensure(8), "staging");
-        d_ui = h->h_uinit.as<double>();
+    const int P = h->host_pipeline;
+    const int64_t chunk = std::min<int64_t>(h->host_chunk, N);
+    const int64_t nchunks = (N + chunk - 1) / chunk;
+    const int used = (int)std::min<int64_t>(P, nchunks);
+    const HostOut o{coef_out, css_ll_out, status_out, n_eval_out, n_grad_out, flags_out};
+    h->host_acc = arima_fit_stats{};
+    // every context the call uses: settle what an earlier call left in it, then size its buffers for a full chunk
+    for (int j = 0; j < used; ++j) {
+        FitCtx &c = h->fctx[j];
+        if (c.has_done) HIPCHK(h, hipEventSynchronize(c.ev_done));
+        c.chunk_n = 0;
+        RCCHK(h, c.d_series.ensure((size_t)chunk * std::max(T, 1) * sizeof(double)), "staging");
+        RCCHK(h, c.d_coef.ensure((size_t)chunk * std::max(k, 1) * sizeof(double)), "staging");
+        RCCHK(h, c.d_ll.ensure((size_t)chunk * sizeof(double)), "staging");
+        RCCHK(h, c.d_status.ensure((size_t)chunk * sizeof(int32_t)), "staging");
+        RCCHK(h, c.d_neval.ensure((size_t)chunk * sizeof(int32_t)), "staging");
+        RCCHK(h, c.d_ngrad.ensure((size_t)chunk * sizeof(int32_t)), "staging");
+        RCCHK(h, c.d_flags.ensure((size_t)chunk), "staging");
+        if (user_init) RCCHK(h, c.d_uinit.ensure((size_t)chunk * std::max(k, 1) * sizeof(double)), "staging");
+        size_t off[6];
+        const size_t need = pin_layout(chunk, k, off);
+        if (c.pin_bytes < need) {
+            if (c.pin) hipHostFree(c.pin);
+            c.pin = nullptr;
+            c.pin_bytes = 0;
+            if (hipHostMalloc(&c.pin, need, 0) != hipSuccess) return set_err(h, ARIMA_E_OOM, "pinned staging");
+            c.pin_bytes = need;
+        }
     }
-    int rc = fit_device_locked(h, h->h_series.as<double>(), N, T, T, p, d, q, I, method, d_ui, h->h_coef.as<double>(),
-                               h->h_ll.as<double>(), h->h_status.as<int32_t>(), h->h_neval.as<int32_t>(),
-                               h->h_ngrad.as<int32_t>(), h->h_flags.as<uint8_t>(), s);
-    if (rc != ARIMA_OK) return rc;
-    if (k > 0) HIPCHK(h, hipMemcpyAsync(coef_out, h->h_coef.ptr, (size_t)N * k * sizeof(double), hipMemcpyDeviceToHost, s));
-    HIPCHK(h, hipMemcpyAsync(css_ll_out, h->h_ll.ptr, (size_t)N * sizeof(double), hipMemcpyDeviceToHost, s));
-    HIPCHK(h, hipMemcpyAsync(status_out, h->h_status.ptr, (size_t)N * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    if (n_eval_out) HIPCHK(h, hipMemcpyAsync(n_eval_out, h->h_neval.ptr, (size_t)N * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    if (n_grad_out) HIPCHK(h, hipMemcpyAsync(n_grad_out, h->h_ngrad.ptr, (size_t)N * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    if (flags_out) HIPCHK(h, hipMemcpyAsync(flags_out, h->h_flags.ptr, (size_t)N, hipMemcpyDeviceToHost, s));
-    HIPCHK(h, end_call(h, s));
-    HIPCHK(h, hipStreamSynchronize(s));
-    return check_fault(h);
+    int rc = ARIMA_OK;
+    for (int64_t j = 0; j < nchunks && rc == ARIMA_OK; ++j) {
+        const int ci = (int)(j % P);
+        FitCtx &c = h->fctx[ci];
+        rc = drain_chunk(h, c, k, o);                       // chunk j - P
+        if (rc != ARIMA_OK) break;
+        const int64_t first = j * chunk, n = std::min(chunk, N - first);
+        hipStream_t s = c.stream;
+        begin_fit(h, c, s);
+        if (T > 0)
+            HIPCHK(h, hipMemcpyAsync(c.d_series.ptr, series + first * T, (size_t)n * T * sizeof(double),
+                                     hipMemcpyHostToDevice, s));
+        const double *d_ui = nullptr;
+        if (user_init) {
+            if (k > 0)
+                HIPCHK(h, hipMemcpyAsync(c.d_uinit.ptr, user_init + first * k, (size_t)n * k * sizeof(double),
+                                         hipMemcpyHostToDevice, s));
+            d_ui = c.d_uinit.as<double>();
+        }
+        rc = fit_device_locked(h, c, ci, used, c.d_series.as<double>(), n, T, T, p, d, q, I, method, d_ui,
+                               c.d_coef.as<double>(), c.d_ll.as<double>(), c.d_status.as<int32_t>(),
+                               c.d_neval.as<int32_t>(), c.d_ngrad.as<int32_t>(), c.d_flags.as<uint8_t>(), s,
+                               nchunks > 1);
+        if (rc == ARIMA_OK) {
+            size_t off[6];
+            pin_layout(n, k, off);
+            char *b = static_cast<char *>(c.pin);
+            if (k > 0) HIPCHK(h, hipMemcpyAsync(b + off[0], c.d_coef.ptr, (size_t)n * k * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(h, hipMemcpyAsync(b + off[1], c.d_ll.ptr, (size_t)n * 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(h, hipMemcpyAsync(b + off[2], c.d_status.ptr, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(h, hipMemcpyAsync(b + off[3], c.d_neval.ptr, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(h, hipMemcpyAsync(b + off[4], c.d_ngrad.ptr, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(h, hipMemcpyAsync(b + off[5], c.d_flags.ptr, (size_t)n, hipMemcpyDeviceToHost, s));
+            c.chunk_first = first;
+            c.chunk_n = n;
+        }
+        HIPCHK(h, end_fit(c, s));
+    }
+    for (int j = 0; j < used; ++j) {                        // the last chunks (every context, even after an error)
+        const int r = drain_chunk(h, h->fctx[j], k, o);
+        if (rc == ARIMA_OK) rc = r;
+    }
+    h->stats = h->host_acc;
+    h->stats_ctx = -1;
+    return rc;
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -718,7 +932,7 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
         return set_err(h, ARIMA_E_INVALID_ARG, "bad search bounds");
     if (max_p > 5 || max_q > 5 || max_d > kMaxD) return set_err(h, ARIMA_E_UNSUPPORTED, "p, q <= 5, d <= 16");
     if (N < 0 || T < 0 || ld < T || !d_order || !d_coef || !d_aic) return set_err(h, ARIMA_E_INVALID_ARG, "bad shape");
-    h->pending = PendingStats{};
+    h->stats_ctx = -1;
     h->stats = arima_fit_stats{};
     if (N == 0) return ARIMA_OK;
     HIPCHK(h, hipSetDevice(h->device));

@@ -384,6 +384,71 @@ def test_long_fits_through_express(engine):
     assert st["express_series"] > 0, st
 
 
+def test_host_path_chunks_match_oracle(engine):
+    # arima_fit_batch cut into 7 chunks over 3 fit contexts (uploads overlapping earlier chunks' fits): every
+    # series bit-identical to the oracle, and the counters summed over the chunks
+    N, T = 2048, 1024
+    s = _device_sample(engine, N, T, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 777).cpu().numpy()
+    engine.set_option("host_chunk", 300)
+    engine.set_option("host_pipeline", 3)
+    try:
+        res = engine.fit_batch(s, 2, 1, 2, True)
+        st_g = engine.stats()
+    finally:
+        engine.set_option("host_chunk", 1 << 18)
+    st, coef, ll, cnt = O.fit_batch(s, 2, 1, 2, 1)
+    exp = dict(status=st, coef=coef, ll=ll, n_eval=cnt[:, 0], n_grad=cnt[:, 1],
+               flags=np.array([O.model_flags(coef[i], 2, 2, 1) if st[i] == 0 else 0 for i in range(N)]))
+    check_fit(res, exp, "host_chunks")
+    assert st_g["n_series"] == N and st_g["n_eval"] == int(cnt[:, 0].sum()), st_g
+
+
+@pytest.mark.parametrize("pipeline", [2, 3])
+def test_pipelined_device_fits_match_serial(engine, pipeline):
+    # fit_pipeline = P: consecutive arima_fit_batch_device calls rotate over P contexts and run concurrently; each
+    # call's outputs must equal the serial run's bit for bit (different orders too, so the contexts differ in shape)
+    import torch
+    N, T = 1 << 16, 1024
+    s = _device_sample(engine, N, T, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 99)
+    orders = [(2, 1, 2, 1), (1, 1, 1, 1), (2, 1, 2, 1), (3, 1, 2, 0), (2, 1, 2, 1)]
+
+    def run(P):
+        engine.set_option("fit_pipeline", P)
+        outs = []
+        try:
+            for (p, d, q, I) in orders:
+                k = p + q + I
+                r = [torch.empty((N, k), dtype=torch.float64, device=s.device),
+                     torch.empty(N, dtype=torch.float64, device=s.device)] + \
+                    [torch.empty(N, dtype=torch.int32, device=s.device) for _ in range(3)] + \
+                    [torch.empty(N, dtype=torch.uint8, device=s.device)]
+                engine.fit_batch_device(s.data_ptr(), N, T, T, p, d, q, I, *[t.data_ptr() for t in r],
+                                        blocking=False)
+                outs.append(r)
+            engine.synchronize()
+        finally:
+            engine.set_option("fit_pipeline", 1)
+        return [[t.cpu().numpy() for t in r] for r in outs]
+
+    a, b = run(1), run(pipeline)
+    for i, (ra, rb) in enumerate(zip(a, b)):
+        for x, y in zip(ra, rb):
+            assert _same(x, y), (pipeline, orders[i])
+
+
+def test_c4_T4096_vs_oracle(engine):
+    # C4 at its own length (BASELINE.json configs[3]): ARIMA(5,1,5)+c, T = 4096, 48 device-generated series checked
+    # against the oracle -- status (MaxEval / bracket failures included), n_eval, n_grad, coefficients, LL, flags
+    N, T = 48, 4096
+    base = [0.1, 0.4, -0.2, 0.1, 0.05, -0.05, 0.3, 0.2, -0.1, 0.05, 0.05]
+    s = _device_sample(engine, N, T, 5, 1, 5, 1, base, 0.02, 20261015).cpu().numpy()
+    res = engine.fit_batch(s, 5, 1, 5, True)
+    st, coef, ll, cnt = O.fit_batch(s, 5, 1, 5, 1)
+    exp = dict(status=st, coef=coef, ll=ll, n_eval=cnt[:, 0], n_grad=cnt[:, 1],
+               flags=np.array([O.model_flags(coef[i], 5, 5, 1) if st[i] == 0 else 0 for i in range(N)]))
+    check_fit(res, exp, "c4_T4096")
+
+
 def test_express_ring_under_pressure_matches_bulk(engine):
     # a small batch of mostly-MaxEval fits: every bulk wave drains early and turns express, so nearly every group of
     # every wave holds a ticket while bulk waves still donate -- the hand-off ring's worst case (a fill must never
