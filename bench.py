@@ -13,7 +13,7 @@ collective; gloo carries only the timing barrier and the max-over-ranks reductio
   --series S        series per GPU (weak scaling, default 1M: configs[1], and configs[2] read per GPU)
   --total-series S  fixed total over all GPUs (strong scaling: configs[2] = 8M series sharded over N GPUs)
   --smear 0|1       Breeze overlap reading at ARIMA.scala:526 (default 1)
-  --pipeline P      fit contexts in rotation (arima_set_option "fit_pipeline", default 2): step i+1's differencing,
+  --pipeline P      fit contexts in rotation (arima_set_option "fit_pipeline", default 3): step i+1's differencing,
                     init and bulk fit run while step i's slowest series finish; every step is still a
                     complete fit of every series, into its own output buffers (one set per context)
   --e2e 0|1         also time one arima_fit_batch call from pageable host memory (default 1)
@@ -136,7 +136,8 @@ def main():
     ap.add_argument("--smear", type=int, default=1, choices=[0, 1])
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (0 = skip)")
     ap.add_argument("--grid-blocks", type=int, default=0)
-    ap.add_argument("--pipeline", type=int, default=2)
+    ap.add_argument("--pipeline", type=int, default=3)
+    ap.add_argument("--express-blocks", type=int, default=-1, help="express workgroups of the fit kernel (-1: CUs/16)")
     ap.add_argument("--e2e", type=int, default=1, choices=[0, 1])
     ap.add_argument("--dry-run", action="store_true")
     args = ap.parse_args()
@@ -196,6 +197,7 @@ def main():
     eng = L.Engine.get(local)
     eng.set_option("smear", args.smear)
     eng.set_option("fit_pipeline", args.pipeline)
+    eng.set_option("express_blocks", args.express_blocks)
     if args.grid_blocks:
         eng.set_option("grid_blocks", args.grid_blocks)
 

@@ -205,6 +205,10 @@ struct alignas(8) FitSlot {
 };
 
 constexpr int kFitWaves = 4;                 // waves per workgroup (one per SIMD)
+#ifndef STS_F_RIDE
+#define STS_F_RIDE 1
+#endif
+constexpr bool kFRide = STS_F_RIDE != 0;     // objective requests fill the idle lanes of gradient passes
 #ifndef STS_OLD_EVALS
 #define STS_OLD_EVALS 128
 #endif
@@ -656,13 +660,16 @@ __global__ __launch_bounds__(64 * kFitWaves, 1) void k_cg_fit(
         const bool doG = nOG != nOF ? nOG > nOF : (nG >= 64 || (nF < 64 && nG >= nF));
         const int rot = (int)(round_no * 37u) & 63;
         round_no++;
+        // A gradient pass also yields the objective, so its lanes left over after the G requests serve objective
+        // requests (tiers 2-3: the request's own point; its predicted points wait for an objective pass).
         int base = 0;
 #pragma unroll
-        for (int tier = 0; tier < 2; ++tier) {
+        for (int tier = 0; tier < (kFRide ? 4 : 2); ++tier) {
+            if (tier >= 2 && (!doG || base >= 64)) break;
 #pragma unroll
             for (int jj = 0; jj < NJ; ++jj) {
                 const int j = (jj + (int)round_no) % NJ;
-                unsigned long long m = (doG ? mG[j] : mF[j]) & (tier == 0 ? mO[j] : ~mO[j]);
+                unsigned long long m = ((doG && tier < 2) ? mG[j] : mF[j]) & ((tier & 1) == 0 ? mO[j] : ~mO[j]);
                 m = (m >> rot) | (rot ? (m << (64 - rot)) : 0ull);          // rotate: lane rot ranks first
                 const int lr = (lane - rot) & 63;
                 if ((m >> lr) & 1ull) {

@@ -81,9 +81,9 @@ def _method_code(method):
     return _lib.METHODS[method]
 
 
-def autofit(ts, maxp=5, maxd=2, maxq=5, sc=None):
-    """ARIMA.autoFit (ARIMA.scala:280-304) is outside this round's hot-path scope."""
-    raise NotImplementedError("autofit: order search is a later row of SURVEY.md 8(f)")
+# ARIMA.autoFit (ARIMA.scala:280-375; python/sparkts/models/ARIMA.py autofit) is deliberately not mirrored: it picks d
+# with the KPSS stationarity test (TimeSeriesStatisticalTests, outside SURVEY.md 8's scope) and then runs a
+# stepwise (p, q, intercept) search. The batched exhaustive grid that covers config C5 is order_search() below.
 
 
 def fit_model(p, d, q, ts, includeIntercept=True, method="css-cgd", userInitParams=None, sc=None, device=None):
@@ -123,6 +123,23 @@ def fit_models(p, d, q, series, includeIntercept=True, method="css-cgd", userIni
     eng = _lib.Engine.get(device)
     r = eng.fit_batch(series, p, d, q, includeIntercept, _method_code(method), userInitParams)
     return FitBatchResult(p, d, q, includeIntercept, r, eng.stats())
+
+
+def order_search(series, maxp=5, maxd=2, maxq=5, intercept_mode=2, device=None):
+    """Config C5: per series, fit every (d <= maxd, p <= maxp, q <= maxq, intercept) and keep
+    the minimum approxAIC (ARIMA.scala:826-830) among fits that returned normally and are stationary and
+    invertible (autoFit's filter, ARIMA.scala:342); ties keep the first in (d, p, q, intercept) order.
+    intercept_mode: 0 = without, 1 = with, 2 = both. Returns a list with an ARIMAModel (or None) per series."""
+    eng = _lib.Engine.get(device)
+    order, coef, _ = eng.order_search(series, maxp, maxd, maxq, intercept_mode)
+    out = []
+    for i in range(order.shape[0]):
+        p, d, q, I = (int(v) for v in order[i])
+        if p < 0:
+            out.append(None)
+        else:
+            out.append(ARIMAModel(p, d, q, coef[i, :p + q + I], bool(I), device=device))
+    return out
 
 
 class ARIMAModel:

@@ -1,5 +1,11 @@
+#!/bin/bash
+# fit-kernel variant comparison (dev libraries, tools/fit_diag.py): LIBS="tag1 tag2 ..." ARGS="..." bash tools/gpu_diag.sh
 set -o pipefail
-mkdir -p gpurun_out/diag
-export SPARKTS_ARIMA_LIB=spark-timeseries_amd/libsparkts_arima_dev_timing.so
-timeout -k 10 120 python tools/fit_diag.py --reps 2 > gpurun_out/diag/timing.json 2> gpurun_out/diag/timing.err &&
-timeout -k 10 120 python tools/fit_diag.py --reps 2 --express-blocks 0 > gpurun_out/diag/timing_x0.json 2> gpurun_out/diag/timing_x0.err
+OUT=gpurun_out/${TAG:-diag}
+mkdir -p $OUT
+for lib in ${LIBS:-timing}; do
+  SPARKTS_ARIMA_LIB=spark-timeseries_amd/libsparkts_arima_dev_$lib.so timeout -k 10 120 python tools/fit_diag.py --reps ${REPS:-2} ${ARGS} > $OUT/$lib.json 2> $OUT/$lib.err
+  rc=$?
+  echo "variant $lib rc=$rc"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+done

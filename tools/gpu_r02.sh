@@ -12,6 +12,9 @@ for step in "$@"; do
     bench_p1) timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 2 --pipeline 1 --e2e 0 --cpu-seconds 0 > $OUT/bench_p1.json 2> $OUT/bench_p1.err ;;
     bench_p3) timeout -k 10 300 python bench.py --steps ${STEPS:-10} --warmup 2 --pipeline 3 --e2e 0 --cpu-seconds 0 > $OUT/bench_p3.json 2> $OUT/bench_p3.err ;;
     bench_c4) timeout -k 10 600 python bench.py --config c4 --series ${C4SER:-131072} --steps 2 --warmup 1 --e2e 0 --cpu-seconds 0 > $OUT/bench_c4.json 2> $OUT/bench_c4.err ;;
+    sweep)    for P in 2 3; do for XB in 16 32 64; do
+                timeout -k 10 200 python bench.py --steps 10 --warmup 2 --pipeline $P --express-blocks $XB --e2e 0 --cpu-seconds 0 > $OUT/sweep_p${P}_x${XB}.json 2> $OUT/sweep_p${P}_x${XB}.err || exit $?
+              done; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   rc=$?
