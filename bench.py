@@ -248,14 +248,31 @@ def main():
     S = n - M
     ff = 2 * (p + q) + 4
     fg = ff + 2 * k * q + 1 + p + q + 2 * k
-    cg_flops = s0["f_passes"] * S * ff + s0["g_passes"] * S * fg
-    cg_ms = s0["ms_cg_fit"]
-    achieved_tf = cg_flops / (cg_ms * 1e-3) / 1e12 if cg_ms > 0 else 0.0
+
+    def cg_flops(st):
+        # U distinct objective points that needed a pass (bulk objective passes, objective requests
+        # served by gradient passes, express objective passes, speculative points the optimizer used), G gradient
+        # passes (without those riders)
+        U = st["f_passes"] + st["ride_passes"] + st["express_f_passes"] + st["spec_hits"]
+        G = st["g_passes"] - st["ride_passes"] + st["express_g_passes"]
+        return U * S * ff + G * S * fg, U, G
+
+    flops_step, U, G = cg_flops(s0)
+    # the dominant kernel's own launch duration: one more step alone on the GPU (fit_pipeline 1), HIP events
+    eng.set_option("fit_pipeline", 1)
+    step()
+    eng.synchronize()
+    s1 = eng.stats()
+    eng.set_option("fit_pipeline", args.pipeline)
+    flops_iso, _, _ = cg_flops(s1)
+    cg_ms = s1["ms_cg_fit"]
+    achieved_tf = flops_iso / (cg_ms * 1e-3) / 1e12 if cg_ms > 0 else 0.0
+    step_tf = flops_step / (elapsed / args.steps) / 1e12
     wave_passes = s0["wave_f_passes"] + s0["wave_g_passes"] + s0["wave_multi_passes"]
     served = s0["f_passes"] + s0["g_passes"]
     lane_util = served / (64.0 * wave_passes) if wave_passes else None
     # HBM bytes the fit kernel streams by construction: one series row per served lane-pass
-    passes_bytes = served * n * 8.0
+    passes_bytes = (served + s0["express_series"]) * n * 8.0
 
     if rank == 0:
         pmc = pmc_traffic({"series": N, "T": T, "p": p, "d": d, "q": q, "I": int(I), "smear": args.smear})
@@ -287,18 +304,29 @@ def main():
                                      "cg_fit": s0["ms_cg_fit"]}},
             "roofline": {"bound": "fp64-valu", "kernel": "k_cg_fit", "achieved": achieved_tf,
                          "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved_tf / FP64_PEAK_TFLOPS,
-                         "achieved_source": "algorithmic flops (SURVEY.md 8(d): U*S*(2(p+q)+4) + G*S*(...), "
-                                            "U, G counted by the kernel) / HIP-event time of the launch",
+                         "launch_ms": cg_ms,
+                         "achieved_source": "algorithmic flops of one k_cg_fit launch (SURVEY.md 8(d): U*S*(2(p+q)+4) "
+                                            "+ G*S*(2(p+q)+4+2kq+1+p+q+2k), U and G counted by the kernel) / that "
+                                            "launch's HIP-event duration, the launch alone on the GPU (one extra "
+                                            "step at fit_pipeline 1 after the timed region)",
+                         "U_per_series": U / max(N, 1), "G_per_series": G / max(N, 1),
+                         "achieved_pipelined": step_tf,
+                         "achieved_pipelined_source": "the timed steps' k_cg_fit algorithmic flops / ms_per_step "
+                                                      "(steady state, launches overlapping)",
                          "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
                          "traffic_unit": "bytes/launch (HBM read+write, rocprofv3 PMC)",
                          "traffic_source": pmc["source"] if pmc else None,
                          "hbm_GBps_pmc": (pmc["hbm_bytes_per_launch"] / (cg_ms * 1e-3) / 1e9) if pmc and cg_ms else None,
                          "hbm_frac_pmc": (pmc["hbm_bytes_per_launch"] / (cg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS)
                          if pmc and cg_ms else None,
+                         "valu_busy_pmc": pmc.get("valu_busy") if pmc else None,
+                         "wait_frac_pmc": pmc.get("wait_frac") if pmc else None,
                          "traffic_model_GBps": passes_bytes / (cg_ms * 1e-3) / 1e9 if cg_ms else None,
                          "hbm_peak_GBps": HBM_PEAK_GBS,
                          "lane_utilisation": lane_util,
                          "spec_hits_per_series": s0["spec_hits"] / max(N, 1),
+                         "ride_passes_per_series": s0["ride_passes"] / max(N, 1),
+                         "express_series": s0["express_series"],
                          "wave_passes": {"f": s0["wave_f_passes"], "g": s0["wave_g_passes"],
                                          "multi": s0["wave_multi_passes"]}},
             "cpu_baseline": None,

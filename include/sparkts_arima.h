@@ -96,6 +96,7 @@ typedef struct arima_fit_stats {
                                 the call also returns ARIMA_E_DEVICE from arima_synchronize / blocking entry points */
     int64_t fault_info[5];   /* the kernel's record of the first fault (ticket, fills, bulk waves done, ...)      */
     int64_t diag[6];         /* diagnostics of builds with -DSTS_TIMING; else 0                       */
+    int64_t ride_passes;     /* objective requests served by gradient passes (counted in g_passes)    */
 } arima_fit_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------------------- */

@@ -62,8 +62,10 @@ __global__ __launch_bounds__(256) void k_hr_init(const double *__restrict__ y, i
     constexpr int KA = K > 0 ? K : 1;
     constexpr int M = P > Q ? P : Q;
     constexpr int m = M + 1;
-    const int64_t sid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (sid >= N) return;
+    // grid-stride over series: a grid smaller than N / 256 blocks bounds the rows in flight (their 2(C_A + C_B)
+    // passes then re-read from the caches instead of HBM)
+    for (int64_t sid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; sid < N;
+         sid += (int64_t)gridDim.x * blockDim.x) {
     const double *row = y + sid * ld;
     int st = hr_shape_status(n, P, Q, I);
     double beta[KA];
@@ -93,6 +95,7 @@ __global__ __launch_bounds__(256) void k_hr_init(const double *__restrict__ y, i
 #pragma unroll
     for (int j = 0; j < K; ++j) init_out[sid * K + j] = beta[j];
     status_out[sid] = st;
+    }
 }
 
 // =======================================================================================================
@@ -534,7 +537,7 @@ __global__ __launch_bounds__(64 * kFitWaves, 1) void k_cg_fit(
     // ctl[0] = work counter, ctl[1] = lane F passes, ctl[2] = lane G passes, ctl[3] = wave F passes (one chain),
     // ctl[4] = wave G passes, ctl[5] = objective evaluations, ctl[6] = gradient evaluations, ctl[7] = spec hits,
     // ctl[8] = wave F passes with speculative chains, ctl[9] = speculative chains evaluated,
-    // ctl[17] = bulk waves started, ctl[20] = express tickets, ctl[21] = express fills (donations),
+    // ctl[17] = bulk waves started, ctl[18] = objective requests served by gradient passes, ctl[20] = express tickets, ctl[21] = express fills (donations),
     // ctl[22] = bulk waves finished,
     // ctl[23] = series finished on the express path, ctl[24] / ctl[25] = express F / G passes
     constexpr int K = I + P + Q;
@@ -559,7 +562,7 @@ __global__ __launch_bounds__(64 * kFitWaves, 1) void k_cg_fit(
     }
     FitSlot<K> *ws = slots[wave];
     unsigned long long lane_f = 0, lane_g = 0, wave_f = 0, wave_g = 0, wave_m = 0, evals = 0, grads = 0, hits = 0,
-                       chains = 0;
+                       chains = 0, rides = 0;
     unsigned round_no = 0;
     bool drained = false;                  // the batch's work counter has run out (this wave saw it)
     const bool lane0 = lane == 0;
@@ -705,6 +708,7 @@ __global__ __launch_bounds__(64 * kFitWaves, 1) void k_cg_fit(
             resp_f = css_to_loglik(css, n);
             wave_g += lane0;
             lane_g += served;
+            rides += (served && S.s.req == REQ_F) ? 1ull : 0ull;
         } else {
             // chains = 1 + the most predictions any served lane posted (wave-uniform)
             const int nsp = served ? (int)S.s.rq_nspec : 0;
@@ -886,6 +890,7 @@ __global__ __launch_bounds__(64 * kFitWaves, 1) void k_cg_fit(
     atomicAdd(&ctl[6], grads);
     atomicAdd(&ctl[7], hits);
     atomicAdd(&ctl[9], chains);
+    atomicAdd(&ctl[18], rides);
 }
 
 // =======================================================================================================
@@ -986,8 +991,12 @@ int launch_hr_init_P(const double *y, int64_t ld, int n, int64_t N, int q, int I
     return with_order(q, [&](auto Qc) {
         return with_bool(I, [&](auto Ic) {
             constexpr int Q = decltype(Qc)::value, II = decltype(Ic)::value;
-            hipLaunchKernelGGL((k_hr_init<P, Q, II>), dim3(grid_for(N, 256)), dim3(256), 0, s, y, ld, n, N, init_out,
-                               status_out);
+#ifdef STS_HR_BLOCKS
+            const unsigned grid = std::min<unsigned>(grid_for(N, 256), STS_HR_BLOCKS);
+#else
+            const unsigned grid = grid_for(N, 256);
+#endif
+            hipLaunchKernelGGL((k_hr_init<P, Q, II>), dim3(grid), dim3(256), 0, s, y, ld, n, N, init_out, status_out);
             STS_CHECK_LAUNCH();
             return ARIMA_OK;
         });

@@ -514,6 +514,7 @@ static void finish_stats(arima_handle *h, FitCtx &c) {
     st.spec_hits = (int64_t)cc[7];
     st.wave_multi_passes = (int64_t)cc[8];
     st.spec_chains = (int64_t)cc[9];
+    st.ride_passes = (int64_t)cc[18];
     st.express_series = (int64_t)cc[23];
     st.express_f_passes = (int64_t)cc[24];
     st.express_g_passes = (int64_t)cc[25];
@@ -533,12 +534,17 @@ static void finish_stats(arima_handle *h, FitCtx &c) {
     const int M = std::max(p, q), m = M + 1;
     if (ps.ar_only) st.hr_passes = N * (int64_t)(2 * (I + p) - I);
     else if (!ps.user_init) st.hr_passes = N * (int64_t)(2 * (1 + m) - 1 + 2 * k - I);
-    // algorithmic flops: U*S*(2(p+q)+4) + G*S*(2(p+q)+4 + 2kq + 1+p+q + 2k) + W_HR
+    // algorithmic flops: U*S*(2(p+q)+4) + G*S*(2(p+q)+4 + 2kq + 1+p+q + 2k) + W_HR, with
+    // U = distinct objective points evaluated by a pass (bulk objective passes, objective requests served by
+    // gradient passes, express objective passes, and the speculative points the optimizer then used) and
+    // G = gradient evaluations that ran a pass (bulk gradient passes without the objective riders, express ones)
     const double S = std::max(n - M, 0);
     const double ff = 2.0 * (p + q) + 4, fg = ff + 2.0 * k * q + 1 + p + q + 2.0 * k;
     const double whr = (double)N * (3.0 * std::max(n - m, 0) * (m + 1) * (m + 1) +
                                     3.0 * std::max(n - 2 * M - 1, 0) * k * k + 2.0 * std::max(n - m, 0) * m);
-    st.flops = (double)st.f_passes * S * ff + (double)st.g_passes * S * fg + (ps.user_init ? 0.0 : whr);
+    const double U = (double)(st.f_passes + st.ride_passes + st.express_f_passes + st.spec_hits);
+    const double G = (double)(st.g_passes - st.ride_passes + st.express_g_passes);
+    st.flops = U * S * ff + G * S * fg + (ps.user_init ? 0.0 : whr);
     st.n_series = N;
     h->stats = st;
     c.pending.valid = false;
@@ -608,6 +614,7 @@ static void acc_stats(arima_fit_stats &a, const arima_fit_stats &s) {
     a.wave_multi_passes += s.wave_multi_passes;
     a.spec_hits += s.spec_hits;
     a.spec_chains += s.spec_chains;
+    a.ride_passes += s.ride_passes;
     a.express_series += s.express_series;
     a.express_f_passes += s.express_f_passes;
     a.express_g_passes += s.express_g_passes;

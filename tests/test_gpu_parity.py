@@ -484,3 +484,23 @@ def test_order_search_T1024_matches_oracle(engine):
     assert np.array_equal(order, eo), (order, eo)
     assert _same(coef, ec)
     assert _same(aic, ea)
+
+
+def test_wire_format_partition_fit_matches_oracle(engine):
+    # records in the JVM <-> Python wire format (PythonConnector.scala:59-88) through fit_arima_records: the
+    # coefficients that come back, decoded, equal the oracle's (NaN for failed fits); two series lengths in one
+    # partition exercise the bucketing
+    from sparkts_amd.timeseriesrdd import bytes_to_key_series, fit_arima_records, key_series_to_bytes
+    rng = np.random.default_rng(31)
+    recs, exp = [], {}
+    for i in range(40):
+        T = 300 if i % 3 else 257
+        y = O.add_time_dependent_effects(rng.standard_normal(T), 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1])
+        y = np.cumsum(y)
+        recs.append(key_series_to_bytes(f"s{i}", y))
+        e = O.fit(y, 2, 1, 2)
+        exp[f"s{i}"] = e["coef"] if e["status"] == 0 else np.full(5, np.nan)
+    out = [bytes_to_key_series(b) for b in fit_arima_records(recs, 2, 1, 2)]
+    assert [k for k, _ in out] == [f"s{i}" for i in range(40)]
+    for k, c in out:
+        assert _same(c, exp[k]), k

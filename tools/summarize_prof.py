@@ -87,9 +87,20 @@ def main():
         import json
         rd = sum(fit["FETCH_SIZE"]) / len(fit["FETCH_SIZE"]) * 1024 * 2
         wr = sum(fit["WRITE_SIZE"]) / len(fit["WRITE_SIZE"]) * 1024
-        json.dump({"workload": {"series": 1048576, "T": 1024, "p": 2, "d": 1, "q": 2, "I": 1},
-                   "kernel": "k_cg_fit", "hbm_bytes_per_launch": rd + wr, "read_bytes": rd, "write_bytes": wr,
-                   "source": source or root}, open(traffic_path, "w"), indent=1)
+        out = {"workload": {"series": 1048576, "T": 1024, "p": 2, "d": 1, "q": 2, "I": 1, "smear": 1},
+               "kernel": "k_cg_fit", "hbm_bytes_per_launch": rd + wr, "read_bytes": rd, "write_bytes": wr,
+               "source": source or root}
+
+        def mean(name):
+            return sum(fit[name]) / len(fit[name]) if name in fit else None
+        wc = mean("SQ_WAVE_CYCLES")
+        if wc:
+            # quad-cycle counters summed over waves; one wave per SIMD, so these are fractions of SIMD time
+            if mean("SQ_ACTIVE_INST_VALU") is not None:
+                out["valu_busy"] = mean("SQ_ACTIVE_INST_VALU") / wc
+            if mean("SQ_WAIT_ANY") is not None:
+                out["wait_frac"] = mean("SQ_WAIT_ANY") / wc
+        json.dump(out, open(traffic_path, "w"), indent=1)
     print(txt)
     if len(sys.argv) > 2:
         open(sys.argv[2], "w").write(txt + "\n")
