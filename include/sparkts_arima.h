@@ -88,7 +88,7 @@ typedef struct arima_fit_stats {
     int64_t spec_hits;       /* objective evaluations answered by a speculative line-search point     */
     int64_t wave_multi_passes; /* wave-level objective passes that carried speculative points          */
     int64_t spec_chains;     /* objective chains evaluated by lane F passes (primary + speculative)    */
-    int64_t express_blocks;  /* express workgroups of the fit kernel (long-running series) */
+    int64_t express_blocks;  /* CUs of express workgroups in the fit kernel (long-running series) */
     int64_t express_series;  /* series finished on the express path                                    */
     int64_t express_f_passes; /* objective / gradient passes run on the express path                    */
     int64_t express_g_passes;

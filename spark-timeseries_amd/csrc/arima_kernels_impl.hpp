@@ -207,7 +207,7 @@ struct alignas(8) FitSlot {
     double pad[kPadWords];
 };
 
-constexpr int kFitWaves = 4;                 // waves per workgroup (one per SIMD)
+constexpr int kFitWaves = kFitBlockWaves;    // waves per workgroup (arima_launch.hpp)
 #ifndef STS_F_RIDE
 #define STS_F_RIDE 1
 #endif
@@ -217,10 +217,11 @@ constexpr bool kFRide = STS_F_RIDE != 0;     // objective requests fill the idle
 #endif
 constexpr int kOldEvals = STS_OLD_EVALS;     // evaluations after which a series is served with priority
 constexpr int kFitLdsBudget = 160 * 1024 - 1024;
-// slots per wave: as many as the LDS holds, at most 2 per lane, a multiple of 8, at least 64
+// slots per wave: as many as the LDS holds, at most 2 per lane, a multiple of 8 (at least 64 unless more than
+// one wave per SIMD shares the LDS)
 template <int K>
 constexpr int fit_slots_per_wave() {
-    constexpr int fit = kFitLdsBudget / (kFitWaves * (int)sizeof(FitSlot<K>));
+    constexpr int fit = kFitLdsBudget / (kFitWavesPerCU * (int)sizeof(FitSlot<K>));
     constexpr int cap = fit > 128 ? 128 : fit;
     return (cap / 8) * 8;
 }
@@ -528,7 +529,7 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
 }
 
 template <int P, int Q, int I, bool SMEAR, int SPW>
-__global__ __launch_bounds__(64 * kFitWaves, 1) void k_cg_fit(
+__global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(kFitWavesPerCU / 4, kFitWavesPerCU / 4))) void k_cg_fit(
     const double *__restrict__ y, int64_t ld, int n, int64_t N, const double *__restrict__ init,
     const int32_t *__restrict__ init_status, double *__restrict__ coef_out, double *__restrict__ ll_out,
     int32_t *__restrict__ status_out, int32_t *__restrict__ n_eval_out, int32_t *__restrict__ n_grad_out,
@@ -543,7 +544,7 @@ __global__ __launch_bounds__(64 * kFitWaves, 1) void k_cg_fit(
     constexpr int K = I + P + Q;
     constexpr int NS = spec_ns<K>();
     constexpr int NJ = (SPW + 63) / 64;      // slot groups: lane l owns slots l, l + 64, ...
-    static_assert(SPW >= 64 && SPW <= 128, "slots per wave");
+    static_assert(SPW >= (kFitWavesPerCU > 4 ? 32 : 64) && SPW <= 128, "slots per wave");
     static_assert(sizeof(FitSlotCore<K>) <= kExpressEntryBytes, "express ring entry");
     __shared__ FitSlot<K> slots[kFitWaves][SPW];
     __shared__ int assign[kFitWaves][64];

@@ -38,6 +38,18 @@ int launch_model_flags(const double *coef, int64_t N, int p, int q, int I, uint8
 int launch_sample(double *out, int64_t ld, int64_t N, int T, int p, int d, int q, int I, const double *base_host,
                   double jitter, uint64_t seed, int64_t first, hipStream_t s);
 int cg_fit_series_per_block(int p, int q, int I);   // optimizer slots of one k_cg_fit workgroup
+// k_cg_fit workgroups are single waves (4 per CU, one per SIMD, each with a quarter of the LDS): a wave that has
+// finished its series leaves the CU at once, so the next fit's waves take its SIMD and LDS share while the other
+// waves of the CU still run their slowest series (pipelined fits)
+#ifndef STS_FIT_BLOCK_WAVES
+#define STS_FIT_BLOCK_WAVES 1
+#endif
+constexpr int kFitBlockWaves = STS_FIT_BLOCK_WAVES;   // waves per k_cg_fit workgroup (1 or 4)
+#ifndef STS_FIT_WAVES_PER_CU
+#define STS_FIT_WAVES_PER_CU 4
+#endif
+constexpr int kFitWavesPerCU = STS_FIT_WAVES_PER_CU;  // resident k_cg_fit waves per CU (4: one per SIMD)
+constexpr int kFitBlocksPerCU = kFitWavesPerCU / kFitBlockWaves;
 
 int hr_shape_status_host(int n, int p, int q, int I);
 int ar_shape_status_host(int n, int p, int I);

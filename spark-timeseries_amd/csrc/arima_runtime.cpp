@@ -406,11 +406,14 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
     }
     // one persistent workgroup per CU (4 waves x the kernel's optimizer slots), the last num_cus/16 of them express
     // workgroups (k_cg_fit's long-series path); fewer bulk blocks when the batch cannot fill them
+    // (express_blocks and grid_blocks count CUs' worth of workgroups: x kFitBlocksPerCU single-wave workgroups)
     const int cus = std::max(1, h->num_cus);
-    int xblocks = h->express_blocks >= 0 ? h->express_blocks : std::max(1, cus / 16);
-    if (xblocks >= cus) xblocks = cus - 1;
-    int blocks = h->grid_blocks_override;
-    if (blocks <= 0) blocks = std::max(1, cus - xblocks);
+    int xcus = h->express_blocks >= 0 ? h->express_blocks : std::max(1, cus / 16);
+    if (xcus >= cus) xcus = cus - 1;
+    int bcus = h->grid_blocks_override;
+    if (bcus <= 0) bcus = std::max(1, cus - xcus);
+    int xblocks = xcus * sts::kFitBlocksPerCU;
+    int blocks = bcus * sts::kFitBlocksPerCU;
     const int per_block = std::max(1, sts::cg_fit_series_per_block(p, q, I));
     const int64_t need = (N + per_block - 1) / per_block;
     if (blocks > need) blocks = (int)need;
@@ -420,7 +423,7 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
         HIPCHK(h, hipMemsetAsync(ws.xready.ptr, 0, sts::kExpressReadyBytes, s));
     }
     *grid_out = blocks;
-    *express_out = xblocks;
+    *express_out = xcus;                    // in CUs, the unit of the "express_blocks" option
     RCCHK(h, sts::launch_cg_fit(y, ldn, n, N, p, q, I, h->smear, init, init_status, d_coef, d_ll, d_status, d_neval,
                                 d_ngrad, d_flags, ws.ctl.as<unsigned long long>(), blocks, xblocks,
                                 ws.xring.as<unsigned char>(), ws.xready.as<unsigned>(), shared_gpu ? 0 : 1, s),
