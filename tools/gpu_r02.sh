@@ -15,6 +15,8 @@ for step in "$@"; do
     sweep)    for P in 2 3; do for XB in 16 32 64; do
                 timeout -k 10 200 python bench.py --steps 10 --warmup 2 --pipeline $P --express-blocks $XB --e2e 0 --cpu-seconds 0 > $OUT/sweep_p${P}_x${XB}.json 2> $OUT/sweep_p${P}_x${XB}.err || exit $?
               done; done ;;
+    search)   timeout -k 10 700 python tools/bench_search.py --series ${SSER:-262144} --lanes ${SLANES:-4} > $OUT/search.json 2> $OUT/search.err ;;
+    prof_c4)  (cd /tmp && export TMPDIR=/tmp; cd "${GRAFT_REPO_ROOT:-/root/repo}" && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_c4 -o run --output-format csv -- python3 bench.py --config c4 --series ${C4SER:-131072} --steps 1 --warmup 1 --pipeline 1 --e2e 0 --cpu-seconds 0 > $OUT/prof_c4.json 2> $OUT/prof_c4.err) ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   rc=$?
