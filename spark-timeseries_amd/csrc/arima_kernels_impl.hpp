@@ -245,7 +245,7 @@ constexpr int fit_slots_per_wave() {
 constexpr int kExpressRing = kExpressRingEntries;
 constexpr int kExpressEntryBytes = 512;      // ring stride reserved per entry (>= sizeof(FitSlotCore<K>) for K <= 11)
 #ifndef STS_EXPRESS_GROUPS
-#define STS_EXPRESS_GROUPS 2
+#define STS_EXPRESS_GROUPS 1
 #endif
 constexpr int kExpressGroups = STS_EXPRESS_GROUPS;   // series per express wave (at most; LDS permitting)
 #ifndef STS_DONATE_EVALS
