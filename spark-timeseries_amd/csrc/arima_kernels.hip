@@ -87,119 +87,189 @@ __global__ __launch_bounds__(256) void k_inverse_difference(const double *__rest
 // Same operations in the same order as the oracle's restatement (oracle/arima_oracle.c orc_forecast), so the
 // result is bit-identical. The final inverseDifferencesOfOrderD over [T-d, T+nFuture) runs in place on the
 // lane's own output row.
+//
+// Memory path (round 2): one wave per workgroup, 64 series. The wave reads its 64 rows as a [64 x kFcCh]
+// tile with coalesced loads (kFcCh consecutive doubles of 64/kFcCh rows per instruction, the next tile
+// prefetched into registers while this one is consumed) and transposes it through LDS, so each lane steps
+// through its own series from LDS. Outputs [0, T-d) go the other way: every lane writes the same output
+// index at the same step (T and d are uniform), into the same LDS ring (the consumed input's column); after each tile the
+// indices no later step can touch (< tile end - d: index x is written at step x or x + d) leave as coalesced
+// row segments. [T-d, T + nFuture) (the diffMatrix diagonal, the forecasts and their re-integration, ≤ 3 % of
+// the bytes) is written by the lane itself, as before.
 // =======================================================================================================
 constexpr int kFcMaxOrder = 5;   // p, q <= 5 (check_orders)
 constexpr int kFcMaxD = 8;
+#ifndef STS_FC_CH
+#define STS_FC_CH 16
+#endif
+constexpr int kFcWave = 64;
+constexpr int kFcCh = STS_FC_CH;                                     // time steps per tile
+constexpr int kFcRing = kFcCh + kFcMaxD;                             // LDS ring columns (>= kFcCh + kFcMaxD)
+constexpr int kFcRowsPerLd = kFcWave / kFcCh;                        // rows per coalesced load instruction
+static_assert(kFcRing >= kFcCh + kFcMaxD, "output ring too small");
+static_assert(kFcWave % kFcCh == 0, "tile width must divide the wave");
 
-__global__ __launch_bounds__(256) void k_forecast(const double *__restrict__ ts_all, int64_t ld_in,
-                                                  const double *__restrict__ coef_all, int k,
-                                                  double *__restrict__ out_all, int64_t ld_out, int64_t N, int T,
-                                                  int p, int d, int q, int I, int nF) {
-    const int64_t sid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (sid >= N) return;
-    const double *ts = ts_all + sid * ld_in;
-    double *out = out_all + sid * ld_out;
-    const int M = p > q ? p : q;
+template <int DD, int MM>
+__global__ __launch_bounds__(kFcWave) void k_forecast(const double *__restrict__ ts_all, int64_t ld_in,
+                                                      const double *__restrict__ coef_all, int k,
+                                                      double *__restrict__ out_all, int64_t ld_out, int64_t N,
+                                                      int T, int p, int q, int I, int nF) {
+    constexpr int d = DD;                                              // d templated: register arrays sized to it
+    constexpr int kD = DD > 0 ? DD : 1;
+    constexpr int kM = MM > 0 ? MM : 1;                                // max(p, q) templated as well
+    // one LDS ring of kFcRing columns per row: the input tile of steps [cb, cb + kFcCh) sits in columns
+    // (cb + u) mod kFcRing; output index x (written at step x or x + d, after input x was consumed) goes to
+    // column x mod kFcRing until it is flushed. Pending outputs [cb - d, cb) and the tile never overlap
+    // because kFcRing >= kFcCh + kFcMaxD.
+    __shared__ double ring[kFcWave][kFcRing + 1];
+    const int lane = (int)threadIdx.x;
+    const int64_t row0 = (int64_t)blockIdx.x * kFcWave;
+    const int64_t sid = row0 + lane;
+    const bool live = sid < N;
+    double *out = out_all + (live ? sid : N - 1) * ld_out;
+    constexpr int M = MM;
     // coefficients [c?, phi_1..phi_p, theta_1..theta_q] (ARIMA.scala:74-77); k == 0 reads nothing
-    const double *cf = coef_all + sid * k;
+    const double *cf = coef_all + (live ? sid : N - 1) * k;
     const double c0 = k > 0 ? cf[0] : 0.0;
-    double phi[kFcMaxOrder], th[kFcMaxOrder];
+    double phi[kM], th[kM];
 #pragma unroll
-    for (int j = 0; j < kFcMaxOrder; ++j) {
+    for (int j = 0; j < MM; ++j) {
         phi[j] = j < p ? cf[I + j] : 0.0;
         th[j] = j < q ? cf[I + p + j] : 0.0;
     }
     const double ia = I ? c0 : 0.0;
-    double xr[kFcMaxOrder], hr[kFcMaxOrder], ma[kFcMaxOrder];
+    double xr[kM], hr[kM], ma[kM];
 #pragma unroll
-    for (int j = 0; j < kFcMaxOrder; ++j) { xr[j] = ia; hr[j] = 0.0; ma[j] = 0.0; }
-    double Dc[kFcMaxD + 1], Dp[kFcMaxD + 1], Mc[kFcMaxD], Mp[kFcMaxD], sr[kFcMaxD + 2];
+    for (int j = 0; j < MM; ++j) { xr[j] = ia; hr[j] = 0.0; ma[j] = 0.0; }
+    double Dc[DD + 1], Dp[DD + 1], Mc[kD], Mp[kD], sr[DD + 2];
 #pragma unroll
-    for (int r = 0; r <= kFcMaxD; ++r) { Dc[r] = 0.0; Dp[r] = 0.0; }
+    for (int r = 0; r <= DD; ++r) { Dc[r] = 0.0; Dp[r] = 0.0; }
 #pragma unroll
-    for (int r = 0; r < kFcMaxD; ++r) { Mc[r] = 0.0; Mp[r] = 0.0; }
+    for (int r = 0; r < kD; ++r) { Mc[r] = 0.0; Mp[r] = 0.0; }
 #pragma unroll
-    for (int j = 0; j < kFcMaxD + 2; ++j) sr[j] = 0.0;
+    for (int j = 0; j < DD + 2; ++j) sr[j] = 0.0;
 
-    for (int t = 0; t < T; ++t) {
-        const double v = ts[t];
-        // differencing column t (UnivariateTimeSeries.scala:384-405 pass r: out(t) = in(t) - in(t-1) for t >= r)
-        Dc[0] = v;
+    const int lim = T - d;                                             // LDS-staged output indices [0, lim)
+    auto put = [&](int idx, double val) {
+        if (idx < lim) ring[lane][idx % kFcRing] = val;   // idx is wave-uniform
+        else if (live) out[idx] = val;
+    };
+    // tile loads: lane reads element tu of row j * kFcRowsPerLd + tr; clamped addresses, so the loads are
+    // unconditional (values outside [0, N) x [0, T) are never consumed)
+    const int tu = lane % kFcCh, tr = lane / kFcCh;
+    double pf[kFcCh];
+    auto load_tile = [&](int cb) {
+        const int t = cb + tu < T ? cb + tu : T - 1;
 #pragma unroll
-        for (int r = 1; r <= kFcMaxD; ++r)
-            if (r <= d) Dc[r] = t < r ? Dc[r - 1] : Dc[r - 1] - Dp[r - 1];
-        // diffMatrix column t and its column sum (d > 0 only)
-        double s = 0.0;
-        if (d > 0) {
-            Mc[0] = v;
-#pragma unroll
-            for (int r = 1; r < kFcMaxD; ++r)
-                if (r < d) Mc[r] = t < r ? 0.0 : (t == r ? Mc[r - 1] : Mc[r - 1] - Mp[r - 1]);
-#pragma unroll
-            for (int r = 0; r < kFcMaxD; ++r)
-                if (r < d) s = s + Mc[r];
-#pragma unroll
-            for (int j = kFcMaxD + 1; j >= 1; --j) sr[j] = sr[j - 1];
-            sr[0] = s;
-#pragma unroll
-            for (int r = 0; r < kFcMaxD; ++r) Mp[r] = Mc[r];
+        for (int j = 0; j < kFcCh; ++j) {
+            const int64_t gi = row0 + j * kFcRowsPerLd + tr;
+            pf[j] = ts_all[(gi < N ? gi : N - 1) * ld_in + t];
         }
+    };
+    int flushed = 0;                                                   // [0, flushed) is in HBM
+    if (T > 0) load_tile(0);
+    for (int cb = 0; cb < T; cb += kFcCh) {
+        __syncthreads();                                               // last tile's reads and flush done
 #pragma unroll
-        for (int r = 0; r <= kFcMaxD; ++r) Dp[r] = Dc[r];
-        if (t < d) out[t] = v;                                       // :724
-        if (t >= d) {
-            // iterateARMA(ext, hist, +, goldStandard = ext) step at ext index M + i, i = t - d (:708, :581-618)
-            const int i = t - d;
-            const double y = Dc[d];
-            double f = 0.0;
-            f = f + (double)I * c0;
+        for (int j = 0; j < kFcCh; ++j) ring[j * kFcRowsPerLd + tr][(cb + tu) % kFcRing] = pf[j];
+        __syncthreads();
+        if (cb + kFcCh < T) load_tile(cb + kFcCh);
+        const int ce = cb + kFcCh < T ? cb + kFcCh : T;
+#pragma unroll 1
+        for (int t = cb; t < ce; ++t) {
+            const double v = ring[lane][t % kFcRing];
+            // differencing column t (UnivariateTimeSeries.scala:384-405 pass r: out(t) = in(t) - in(t-1) for t >= r)
+            Dc[0] = v;
 #pragma unroll
-            for (int j = 0; j < kFcMaxOrder; ++j)
-                if (j < p) f = f + xr[j] * phi[j];
+            for (int r = 1; r <= DD; ++r)
+                if (r <= d) Dc[r] = t < r ? Dc[r - 1] : Dc[r - 1] - Dp[r - 1];
+            // diffMatrix column t and its column sum (d > 0 only)
+            double s = 0.0;
+            if (d > 0) {
+                Mc[0] = v;
 #pragma unroll
-            for (int j = 0; j < kFcMaxOrder; ++j)
-                if (j < q) f = f + ma[j] * th[j];
-            const double err = y - f;
+                for (int r = 1; r < DD; ++r)
+                    if (r < d) Mc[r] = t < r ? 0.0 : (t == r ? Mc[r - 1] : Mc[r - 1] - Mp[r - 1]);
 #pragma unroll
-            for (int j = kFcMaxOrder - 1; j >= 1; --j)                 // updateMAErrors (:544-554): smear
-                if (j < q) ma[j] = ma[0];
-            if (q > 0) ma[0] = err;
+                for (int r = 0; r < kD; ++r)
+                    if (r < d) s = s + Mc[r];
 #pragma unroll
-            for (int j = kFcMaxOrder - 1; j >= 1; --j) { xr[j] = xr[j - 1]; hr[j] = hr[j - 1]; }
-            xr[0] = y;
-            hr[0] = f;
-            if (d == 0) {
-                out[i] = f;                                            // :726
-            } else if (i >= d && i < T - d) {
-                double sd = 0.0;                                       // column sum at i - 1 = t - d - 1
+                for (int j = DD + 1; j >= 1; --j) sr[j] = sr[j - 1];
+                sr[0] = s;
 #pragma unroll
-                for (int j = 0; j < kFcMaxD + 2; ++j)
-                    if (j == d + 1) sd = sr[j];
-                out[i] = sd + f;                                       // :745-751
+                for (int r = 0; r < kD; ++r) Mp[r] = Mc[r];
+            }
+#pragma unroll
+            for (int r = 0; r <= DD; ++r) Dp[r] = Dc[r];
+            if (t < d) put(t, v);                                      // :724
+            if (t >= d) {
+                // iterateARMA(ext, hist, +, goldStandard = ext) step at ext index M + i, i = t - d (:708, :581-618)
+                const int i = t - d;
+                const double y = Dc[d];
+                double f = 0.0;
+                f = f + (double)I * c0;
+#pragma unroll
+                for (int j = 0; j < MM; ++j)
+                    if (j < p) f = f + xr[j] * phi[j];
+#pragma unroll
+                for (int j = 0; j < MM; ++j)
+                    if (j < q) f = f + ma[j] * th[j];
+                const double err = y - f;
+#pragma unroll
+                for (int j = MM - 1; j >= 1; --j)             // updateMAErrors (:544-554): smear
+                    if (j < q) ma[j] = ma[0];
+                if (q > 0) ma[0] = err;
+#pragma unroll
+                for (int j = MM - 1; j >= 1; --j) { xr[j] = xr[j - 1]; hr[j] = hr[j - 1]; }
+                xr[0] = y;
+                hr[0] = f;
+                if (d == 0) {
+                    put(i, f);                                         // :726
+                } else if (i >= d && i < T - d) {
+                    double sd = 0.0;                                   // column sum at i - 1 = t - d - 1
+#pragma unroll
+                    for (int j = 0; j < DD + 2; ++j)
+                        if (j == d + 1) sd = sr[j];
+                    put(i, sd + f);                                    // :745-751
+                }
+            }
+            if (d > 0 && t >= T - d) {                                 // diag(diffMatrix(0 until d, -d to -1))
+                const int r = t - (T - d);
+                double dg = 0.0;
+#pragma unroll
+                for (int j = 0; j < DD; ++j)
+                    if (j == r) dg = Mc[j];
+                put(t, dg);
             }
         }
-        if (d > 0 && t >= T - d) {                                     // diag(diffMatrix(0 until d, -d to -1))
-            const int r = t - (T - d);
-            double dg = 0.0;
+        __syncthreads();                                               // ring entries of every lane written
+        const int fe = ce - d < lim ? ce - d : lim;                    // indices < fe are final
+        if (fe > flushed) {
+            const int idx = flushed + tu;
+            if (idx < fe) {
 #pragma unroll
-            for (int j = 0; j < kFcMaxD; ++j)
-                if (j == r) dg = Mc[j];
-            out[t] = dg;
+                for (int j = 0; j < kFcCh; ++j) {
+                    const int r = j * kFcRowsPerLd + tr;
+                    if (row0 + r < N) out_all[(row0 + r) * ld_out + idx] = ring[r][idx % kFcRing];
+                }
+            }
+            flushed = fe;
         }
     }
+    if (!live) return;
     // forward = hist(-M..) ++ zeros(nFuture); iterateARMA(forward, forward, +, gold = forward, maTerms) (:711-720)
-    double fr[kFcMaxOrder], mt[kFcMaxOrder];
+    double fr[kM], mt[kM];
 #pragma unroll
-    for (int j = 0; j < kFcMaxOrder; ++j) {
+    for (int j = 0; j < MM; ++j) {
         fr[j] = hr[j];                                                 // fwd(i-1-j)
         mt[j] = 0.0;
     }
 #pragma unroll
-    for (int j = 0; j < kFcMaxOrder; ++j)                              // maTerms(j) = ext(L-M+j) - hist(L-M+j)
+    for (int j = 0; j < MM; ++j)                              // maTerms(j) = ext(L-M+j) - hist(L-M+j)
         if (j < M) {
             double xv = 0.0, hv = 0.0;
 #pragma unroll
-            for (int jj = 0; jj < kFcMaxOrder; ++jj)
+            for (int jj = 0; jj < MM; ++jj)
                 if (jj == M - 1 - j) { xv = xr[jj]; hv = hr[jj]; }
             mt[j] = xv - hv;
         }
@@ -208,18 +278,18 @@ __global__ __launch_bounds__(256) void k_forecast(const double *__restrict__ ts_
         double f = 0.0;
         f = f + (double)I * c0;
 #pragma unroll
-        for (int j = 0; j < kFcMaxOrder; ++j)
+        for (int j = 0; j < MM; ++j)
             if (j < p) f = f + fr[j] * phi[j];
 #pragma unroll
-        for (int j = 0; j < kFcMaxOrder; ++j)
+        for (int j = 0; j < MM; ++j)
             if (j < q) f = f + mt[j] * th[j];
         const double err = f - f;
 #pragma unroll
-        for (int j = kFcMaxOrder - 1; j >= 1; --j)                     // updateMAErrors over maTerms' length M
+        for (int j = MM - 1; j >= 1; --j)                     // updateMAErrors over maTerms' length M
             if (j < M) mt[j] = mt[0];
         if (M > 0) mt[0] = err;
 #pragma unroll
-        for (int j = kFcMaxOrder - 1; j >= 1; --j) fr[j] = fr[j - 1];
+        for (int j = MM - 1; j >= 1; --j) fr[j] = fr[j - 1];
         fr[0] = f;
         fo[i] = f;                                                     // :728
     }
@@ -403,8 +473,21 @@ int launch_forecast(const double *ts, int64_t ld_in, const double *coef, int k, 
     if (N == 0) return ARIMA_OK;
     if (p > kFcMaxOrder || q > kFcMaxOrder || d > kFcMaxD) return ARIMA_E_UNSUPPORTED;
     if (T < d || n_future < 0 || k != I + p + q || ld_out < (int64_t)T + n_future) return ARIMA_E_INVALID_ARG;
-    hipLaunchKernelGGL(k_forecast, dim3(grid_for(N, 256)), dim3(256), 0, s, ts, ld_in, coef, k, out, ld_out, N, T,
-                       p, d, q, I, n_future);
+    const dim3 grid(grid_for(N, kFcWave)), block(kFcWave);
+    const int M = p > q ? p : q;
+    switch (d * (kFcMaxOrder + 1) + M) {
+#define STS_FC_CASE(D, MM)                                                                                          \
+    case D * (kFcMaxOrder + 1) + MM:                                                                                \
+        hipLaunchKernelGGL((k_forecast<D, MM>), grid, block, 0, s, ts, ld_in, coef, k, out, ld_out, N, T, p, q, I, \
+                           n_future);                                                                               \
+        break;
+#define STS_FC_CASES(D) STS_FC_CASE(D, 0) STS_FC_CASE(D, 1) STS_FC_CASE(D, 2) STS_FC_CASE(D, 3) STS_FC_CASE(D, 4)    \
+    STS_FC_CASE(D, 5)
+    STS_FC_CASES(0) STS_FC_CASES(1) STS_FC_CASES(2) STS_FC_CASES(3) STS_FC_CASES(4) STS_FC_CASES(5) STS_FC_CASES(6)
+    STS_FC_CASES(7) STS_FC_CASES(8)
+#undef STS_FC_CASES
+#undef STS_FC_CASE
+    }
     STS_CHECK_LAUNCH();
     return ARIMA_OK;
 }

@@ -219,6 +219,31 @@ def test_forecast_bit_exact(engine, pdqi, n_future):
     assert _same(out, exp), (pdqi, n_future, np.nanmax(np.abs(out - exp)))
 
 
+@pytest.mark.parametrize("pdqi", [(0, 4, 0, 1), (2, 5, 1, 0), (1, 6, 4, 1), (5, 7, 3, 1), (4, 0, 5, 0), (3, 1, 0, 1)])
+@pytest.mark.parametrize("N", [1, 65])
+def test_forecast_tiles_ragged(engine, pdqi, N):
+    # k_forecast works on 64-series x 16-step LDS tiles (one instantiation per (d, max(p, q))): partial waves,
+    # a length that is no multiple of the tile, d up to 7 (output lag d inside the LDS ring), and strided rows
+    # (ld > T) through the device entry point
+    import torch
+    p, d, q, I = pdqi
+    rng = np.random.default_rng(77 + 11 * d + p + N)
+    T, nf, ld, ldo = 37, 9, 45, 50
+    s = rng.standard_normal((N, T)).cumsum(axis=1) + 2.0
+    coef = rng.uniform(-0.5, 0.5, (N, p + q + I))
+    exp = np.stack([O.forecast(s[i], p, d, q, I, coef[i], nf) for i in range(N)])
+    assert _same(engine.forecast(s, p, d, q, I, coef, nf), exp)
+    sd = torch.zeros((N, ld), dtype=torch.float64, device="cuda")
+    sd[:, :T] = torch.from_numpy(s).cuda()
+    cd = torch.from_numpy(coef).cuda().contiguous()
+    od = torch.full((N, ldo), -7.0, dtype=torch.float64, device="cuda")
+    engine.forecast_device(sd.data_ptr(), N, T, ld, p, d, q, I, cd.data_ptr(), nf, od.data_ptr(), ldo)
+    torch.cuda.synchronize()
+    o = od.cpu().numpy()
+    assert _same(o[:, :T + nf], exp)
+    assert np.all(o[:, T + nf:] == -7.0)                     # nothing written past T + nFuture
+
+
 @pytest.mark.parametrize("T", [2, 3, 4, 6])
 def test_forecast_short_series(engine, T):
     # series barely longer than d and shorter than max(p, q): the prefix/diag regions overlap (C-9 edge cases)

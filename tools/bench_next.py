@@ -57,6 +57,9 @@ def main():
 
     # order search (C5 grid)
     N = a.os_series
+    if N <= 0:
+        print(json.dumps(out))
+        return
     s = torch.empty((N, T), dtype=torch.float64, device=dev)
     eng.sample_device(s.data_ptr(), N, T, T, 2, 1, 2, True, base, 0.05, 20261015)
     order = torch.empty((N, 4), dtype=torch.int32, device=dev)
