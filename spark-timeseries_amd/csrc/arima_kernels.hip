@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void k_inverse_difference(const double *__rest
 constexpr int kFcMaxOrder = 5;   // p, q <= 5 (check_orders)
 constexpr int kFcMaxD = 8;
 #ifndef STS_FC_CH
-#define STS_FC_CH 16
+#define STS_FC_CH 32
 #endif
 constexpr int kFcWave = 64;
 constexpr int kFcCh = STS_FC_CH;                                     // time steps per tile
