@@ -117,7 +117,7 @@ struct arima_handle {
     int express_blocks = -1;       // k_cg_fit express workgroups (-1: num_cus / 16)
     int64_t last_express = 0;
     int64_t last_grid = 0;
-    int search_lanes = 4;          // concurrent fits of the order search
+    int search_lanes = 8;          // concurrent fits of the order search (2/4/8: 1269/1303/1408 series/s, profiles/r02/g_c5)
     int pipeline = 1;              // fit contexts in rotation (option "fit_pipeline")
     int host_pipeline = 3;         // contexts the chunked host path rotates over
     int64_t host_chunk = 1 << 18;  // series per chunk of the host path (option "host_chunk")

@@ -18,7 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--series", type=int, default=1 << 18)
     ap.add_argument("--T", type=int, default=1024)
-    ap.add_argument("--lanes", type=int, default=4)
+    ap.add_argument("--lanes", type=int, default=8)
     a = ap.parse_args()
     import torch
     import sparkts_amd._lib as L
