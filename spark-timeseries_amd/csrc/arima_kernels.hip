@@ -99,6 +99,9 @@ __global__ __launch_bounds__(256) void k_inverse_difference(const double *__rest
 // =======================================================================================================
 constexpr int kFcMaxOrder = 5;   // p, q <= 5 (check_orders)
 constexpr int kFcMaxD = 8;
+#ifndef STS_FC_NT
+#define STS_FC_NT 0                                                   // non-temporal tile loads / flush stores
+#endif
 #ifndef STS_FC_CH
 #define STS_FC_CH 32
 #endif
@@ -163,7 +166,11 @@ __global__ __launch_bounds__(kFcWave) void k_forecast(const double *__restrict__
 #pragma unroll
         for (int j = 0; j < kFcCh; ++j) {
             const int64_t gi = row0 + j * kFcRowsPerLd + tr;
+#if STS_FC_NT
+            pf[j] = __builtin_nontemporal_load(ts_all + (gi < N ? gi : N - 1) * ld_in + t);
+#else
             pf[j] = ts_all[(gi < N ? gi : N - 1) * ld_in + t];
+#endif
         }
     };
     int flushed = 0;                                                   // [0, flushed) is in HBM
@@ -250,7 +257,12 @@ __global__ __launch_bounds__(kFcWave) void k_forecast(const double *__restrict__
 #pragma unroll
                 for (int j = 0; j < kFcCh; ++j) {
                     const int r = j * kFcRowsPerLd + tr;
+#if STS_FC_NT
+                    if (row0 + r < N)
+                        __builtin_nontemporal_store(ring[r][idx % kFcRing], out_all + (row0 + r) * ld_out + idx);
+#else
                     if (row0 + r < N) out_all[(row0 + r) * ld_out + idx] = ring[r][idx % kFcRing];
+#endif
                 }
             }
             flushed = fe;
