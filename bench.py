@@ -17,6 +17,9 @@ collective; gloo carries only the timing barrier and the max-over-ranks reductio
                     init and bulk fit run while step i's slowest series finish; every step is still a
                     complete fit of every series, into its own output buffers (one set per context)
   --e2e 0|1         also time one arima_fit_batch call from pageable host memory (default 1)
+  --config c5       BASELINE.json configs[4]: a step = the full (d <= 2, p <= 5, q <= 5, +-c) min-approxAIC order search
+                    over this rank's shard (strong scaling over --total-series, default 1M); unit series searched/sec
+  --device D        bind every rank to GPU D (also SPARKTS_DEVICE) instead of LOCAL_RANK's: several ranks on one GPU
   --dry-run         no GPU: ranks compute their shards and report (tests/test_multirank.py)
 Prints ONE JSON line on rank 0.
 """
@@ -32,7 +35,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "spark-timeseries_amd"))
 
 CONFIGS = {
-    # name: (p, d, q, intercept, T, base coefficients, jitter)
+    # name: (p, d, q, intercept, T, base coefficients, jitter); c5 searches over C2-shaped series
+    "c5": (2, 1, 2, 1, 1024, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05),
     "c2": (2, 1, 2, 1, 1024, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05),
     "c1": (1, 0, 1, 1, 500, [3.5, 0.3, 0.7], 0.05),
     "c4": (5, 1, 5, 1, 4096, [0.1, 0.4, -0.2, 0.1, 0.05, -0.05, 0.3, 0.2, -0.1, 0.05, 0.05], 0.02),
@@ -44,16 +48,53 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md)
 # tools/summarize_prof.py --traffic). Counters cannot be read inside a timed bench run, so the measured value
 # is carried in this tracked file and reported only when its workload (and build tag) matches the one run.
 PMC_TRAFFIC_FILE = os.path.join(ROOT, "tools", "pmc_traffic_c2.json")
+LIB_PATH = os.path.join(ROOT, "spark-timeseries_amd", "libsparkts_arima.so")
 SEED = 20261015
 
 
-def pmc_traffic(workload):
+def build_sha():
+    """sha256 of the HIP library this run loads: the key that ties carried PMC numbers to the measured build."""
+    import hashlib
+    h = hashlib.sha256()
+    try:
+        with open(os.environ.get("SPARKTS_ARIMA_LIB", LIB_PATH), "rb") as f:
+            for blk in iter(lambda: f.read(1 << 22), b""):
+                h.update(blk)
+    except OSError:
+        return None
+    return h.hexdigest()
+
+
+def pmc_traffic(workload, sha):
+    """Carried PMC record of this workload AND this build (library sha256); None for any mismatch."""
     try:
         with open(PMC_TRAFFIC_FILE) as f:
-            m = json.load(f)
+            recs = json.load(f)
     except (OSError, ValueError):
         return None
-    return m if m.get("workload") == workload else None
+    for m in recs if isinstance(recs, list) else [recs]:
+        if m.get("workload") == workload and sha is not None and m.get("build_sha") == sha:
+            return m
+    return None
+
+
+def physical_cores():
+    """Physical cores of the host (unique (package, core) pairs of /proc/cpuinfo), or None."""
+    try:
+        pairs, phys, core = set(), None, None
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("physical id"):
+                    phys = line.split(":")[1].strip()
+                elif line.startswith("core id"):
+                    core = line.split(":")[1].strip()
+                elif not line.strip():
+                    if phys is not None and core is not None:
+                        pairs.add((phys, core))
+                    phys = core = None
+        return len(pairs) or None
+    except OSError:
+        return None
 
 
 def log(*a):
@@ -79,7 +120,8 @@ def launch_ranks(n):
 
 
 def cpu_baseline(series_host, p, d, q, I, smear, target_s):
-    """The CPU restatement (oracle/, kind "port") on a bounded sample, OpenMP over this rank's CPU share.
+    """The CPU restatement (oracle/, kind "port") on a bounded sample: OpenMP over this rank's CPU share (the lease's
+    threads), then the same sample on ONE core, so the figure can be read per core.
 
     The sample (the first rows of rank 0's shard) is fitted repeatedly until ~target_s seconds have passed."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -88,26 +130,38 @@ def cpu_baseline(series_host, p, d, q, I, smear, target_s):
     omp_env = os.environ.get("OMP_NUM_THREADS")
     cores = int(omp_env or "0") or affinity
     cores = max(1, min(cores, affinity, 64))
-    os.environ["OMP_NUM_THREADS"] = str(cores)
+
+    def timed(threads, sample, budget):
+        os.environ["OMP_NUM_THREADS"] = str(threads)
+        O.set_threads(threads)
+        done, rounds, conv = 0, 0, 0
+        t0 = time.perf_counter()
+        while True:
+            st, _, _, _ = O.fit_batch(sample, p, d, q, I, smear=smear)
+            done += len(sample)
+            rounds += 1
+            conv = int((st == 0).sum())
+            if time.perf_counter() - t0 >= budget:
+                break
+        return done / (time.perf_counter() - t0), rounds, conv
+
     O.lib()
-    sample = series_host
-    done, rounds, conv = 0, 0, 0
-    t0 = time.perf_counter()
-    while True:
-        st, _, _, _ = O.fit_batch(sample, p, d, q, I, smear=smear)
-        done += len(sample)
-        rounds += 1
-        conv = int((st == 0).sum())
-        if time.perf_counter() - t0 >= target_s:
-            break
-    dt = time.perf_counter() - t0
-    return {"value": done / dt, "unit": "series fitted/sec", "cores": cores, "kind": "port",
-            "host_cpus": os.cpu_count(), "affinity_cpus": affinity,
-            "sample": f"{len(sample)} synthetic series of the benchmark workload (first rows of rank 0's shard) "
-                      f"fitted {rounds}x in {dt:.1f} s by the C restatement oracle/arima_oracle.c "
-                      f"(OpenMP, {cores} threads: OMP_NUM_THREADS={omp_env}, the lease's CPU share; this process "
-                      f"may run on {affinity} CPUs and the box reports {os.cpu_count()} in all; "
-                      f"{conv}/{len(sample)} converged); not the spark-ts JVM"}
+    rate, rounds, conv = timed(cores, series_host, target_s)
+    one = series_host[: max(1, len(series_host) // 16)]
+    rate1, rounds1, _ = timed(1, one, max(2.0, target_s / 3))
+    os.environ["OMP_NUM_THREADS"] = str(cores)
+    O.set_threads(cores)
+    phys = physical_cores()
+    return {"value": rate, "unit": "series fitted/sec", "cores": cores, "kind": "port",
+            "value_1core": rate1, "host_physical_cores": phys, "host_cpus": os.cpu_count(), "affinity_cpus": affinity,
+            "projected_all_physical_cores": rate1 * phys if phys else None,
+            "sample": f"{len(series_host)} synthetic series of the benchmark workload (first rows of rank 0's shard) "
+                      f"fitted {rounds}x by the C restatement oracle/arima_oracle.c with {cores} OpenMP threads "
+                      f"(OMP_NUM_THREADS={omp_env}: the lease's CPU share; {affinity} CPUs in this process's affinity, "
+                      f"{os.cpu_count()} CPUs / {phys} physical cores on the host); {conv}/{len(series_host)} converged; "
+                      f"value_1core: the first {len(one)} of them {rounds1}x on one thread; "
+                      f"projected_all_physical_cores = value_1core x physical cores (linear, not measured); "
+                      f"not the spark-ts JVM"}
 
 
 def end_to_end(eng, series, p, d, q, I):
@@ -139,8 +193,11 @@ def main():
     ap.add_argument("--pipeline", type=int, default=3)
     ap.add_argument("--express-blocks", type=int, default=-1, help="express workgroups of the fit kernel (-1: CUs/16)")
     ap.add_argument("--e2e", type=int, default=1, choices=[0, 1])
+    ap.add_argument("--device", type=int, default=None, help="GPU of every rank (default: LOCAL_RANK's)")
     ap.add_argument("--dry-run", action="store_true")
     args = ap.parse_args()
+    if args.device is not None:
+        os.environ["SPARKTS_DEVICE"] = str(args.device)
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
@@ -154,15 +211,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev_id = int(os.environ["SPARKTS_DEVICE"]) if os.environ.get("SPARKTS_DEVICE", "") != "" else local
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if world > 1:
         if not args.dry_run:
-            torch.cuda.set_device(local)
+            torch.cuda.set_device(dev_id)
         # the data path has no collective; gloo (CPU) carries only the timing barrier and max-reduction
         dist.init_process_group("gloo")
 
     p, d, q, I, T, base, jitter = CONFIGS[args.config]
+    if args.config == "c5" and not args.total_series:
+        args.total_series = 1 << 20                 # configs[4]: 1M series over the node's GPUs
     if args.total_series:
         first, last = shard_range(args.total_series, rank, world)     # strong scaling: fixed total
         scaling = "strong"
@@ -193,8 +253,8 @@ def main():
         return
 
     import sparkts_amd._lib as L
-    dev = torch.device("cuda", local)
-    eng = L.Engine.get(local)
+    dev = torch.device("cuda", dev_id)
+    eng = L.Engine.get(dev_id)
     eng.set_option("smear", args.smear)
     eng.set_option("fit_pipeline", args.pipeline)
     eng.set_option("express_blocks", args.express_blocks)
@@ -203,6 +263,8 @@ def main():
 
     series = torch.empty((N, T), dtype=torch.float64, device=dev)
     eng.sample_device(series.data_ptr(), N, T, T, p, d, q, I, base, jitter, SEED, first)
+    if args.config == "c5":
+        return run_c5(args, eng, series, N, T, total_series, world, rank, dev, barrier, dist, max_over_ranks, scaling)
     # one output set per fit context: pipelined steps never write the same buffers concurrently
     outs = [dict(coef=torch.empty((N, k), dtype=torch.float64, device=dev),
                  ll=torch.empty(N, dtype=torch.float64, device=dev),
@@ -275,7 +337,8 @@ def main():
     passes_bytes = (served + s0["express_series"]) * n * 8.0
 
     if rank == 0:
-        pmc = pmc_traffic({"series": N, "T": T, "p": p, "d": d, "q": q, "I": int(I), "smear": args.smear})
+        sha = build_sha()
+        pmc = pmc_traffic({"series": N, "T": T, "p": p, "d": d, "q": q, "I": int(I), "smear": args.smear}, sha)
         result = {
             "metric": "series fitted/sec, ARIMA(2,1,2) CSS-CGD, 1M x 1024 pts" if args.config == "c2"
             else f"series fitted/sec, {args.config}",
@@ -315,7 +378,9 @@ def main():
                                                       "(steady state, launches overlapping)",
                          "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
                          "traffic_unit": "bytes/launch (HBM read+write, rocprofv3 PMC)",
-                         "traffic_source": pmc["source"] if pmc else None,
+                         "traffic_source": pmc["source"] if pmc else
+                         "no rocprofv3 PMC record of this workload for this build (library sha256 " + str(sha)[:16] + ")",
+                         "build_sha": sha,
                          "hbm_GBps_pmc": (pmc["hbm_bytes_per_launch"] / (cg_ms * 1e-3) / 1e9) if pmc and cg_ms else None,
                          "hbm_frac_pmc": (pmc["hbm_bytes_per_launch"] / (cg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS)
                          if pmc and cg_ms else None,
@@ -337,6 +402,73 @@ def main():
             host = series[: 4096].cpu().numpy()
             result["cpu_baseline"] = cpu_baseline(host, p, d, q, I, args.smear, args.cpu_seconds)
         print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run_c5(args, eng, series, N, T, total_series, world, rank, dev, barrier, dist, max_over_ranks, scaling):
+    """configs[4]: a step = the full (d <= 2, p <= 5, q <= 5, +-c) order search (216 fits per series, min approxAIC
+    among stationary and invertible fits, ARIMA.scala:826-830 / :342) over this rank's shard, device-resident."""
+    import torch
+    order = torch.empty((max(N, 1), 4), dtype=torch.int32, device=dev)
+    coef = torch.empty((max(N, 1), 11), dtype=torch.float64, device=dev)
+    aic = torch.empty(max(N, 1), dtype=torch.float64, device=dev)
+
+    def step():
+        import threading
+        eng.order_search_device(series.data_ptr(), N, T, T, 5, 2, 5, 2, order.data_ptr(), coef.data_ptr(),
+                                aic.data_ptr(), blocking=False)
+        done = threading.Event()
+        t0 = time.perf_counter()
+
+        def progress():                    # a full-size search runs for minutes: a line every 30 s
+            while not done.wait(30):
+                log(f"[rank {rank}] searching ... {time.perf_counter() - t0:.0f} s")
+        th = threading.Thread(target=progress, daemon=True)
+        th.start()
+        try:
+            eng.synchronize()
+        finally:
+            done.set()
+            th.join()
+
+    for i in range(args.warmup):
+        step()
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step()
+        log(f"[rank {rank}] search step {i} done at {time.perf_counter() - t0:.1f} s")
+    torch.cuda.synchronize(dev)
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, dist if world > 1 else None)
+    o = order[:N].cpu().numpy()
+    found = float((o[:, 0] >= 0).mean()) if N else 1.0
+    if rank == 0:
+        sel = {}
+        for r in o[: min(N, 65536)]:
+            key = f"({r[0]},{r[1]},{r[2]}){'+c' if r[3] == 1 else ''}" if r[0] >= 0 else "none"
+            sel[key] = sel.get(key, 0) + 1
+        print(json.dumps({
+            "metric": "series searched/sec, ARIMA order search p,q<=5 d<=2 +-c (216 CSS-CGD fits/series, min approxAIC), "
+                      "x 1024 pts",
+            "value": total_series * args.steps / elapsed, "unit": "series searched/sec", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f64",
+            "data": f"synthetic C2-shaped series (ARIMAModel.sample semantics on device, seed {SEED})",
+            "config": {"workload": f"order search over {total_series} series x {T} pts "
+                                   f"({'total over ' + str(world) + ' GPU(s)' if scaling == 'strong' else 'per GPU'};"
+                                   f" BASELINE.json configs[4])",
+                       "series_per_gpu": N, "series_total": total_series, "fits_per_series": 216,
+                       "fits_per_sec": total_series * 216 * args.steps / elapsed, "search_lanes": 8,
+                       "found_fraction": found, "selected_orders_top":
+                           dict(sorted(sel.items(), key=lambda kv: -kv[1])[:6]),
+                       "parallelism": f"series-sharded x{world}, no collective"},
+            "roofline": None,
+            "roofline_note": "per grid point (flops, evaluations, MaxEval fraction): tools/grid_profile.py",
+            "cpu_baseline": None}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -286,14 +286,34 @@ int orc_ols(const double *Y, const double *X, int rows, int ncx, int intercept, 
     return ARIMA_ST_OK;
 }
 
+/* Lag.lagMatTrimBoth(x, maxLag, includeOriginal)  Lag.scala:33-49 (Array[Array[Double]] form, row-major out:
+ * rows n - maxLag, cols maxLag (+1); lagMat(r)(c - initialLag) = x(r + maxLag - c) for c = initialLag..maxLag) */
+static void lag_mat_trim_both(const double *x, int n, int maxLag, int includeOriginal, double *out) {
+    const int rows = n - maxLag, cols = maxLag + (includeOriginal ? 1 : 0), initialLag = includeOriginal ? 0 : 1;
+    for (int r = 0; r < rows; r++)
+        for (int c = initialLag; c <= maxLag; c++) out[(size_t)r * cols + (c - initialLag)] = x[r + maxLag - c];
+}
+
+/* UnivariateTimeSeries.lag(ts, maxLag, includeOriginal) = Lag.lagMatTrimBoth(Vector, ...)  Lag.scala:62-99:
+ * the same matrix as a column-major DenseMatrix (numTruncatedRows = x.size - numRows = maxLag). Returns rows. */
+int orc_lag_matrix(const double *x, int n, int maxLag, int includeOriginal, double *out_colmajor) {
+    const int rows = n - maxLag, cols = maxLag + (includeOriginal ? 1 : 0);
+    if (rows < 0) return -1;
+    double *rm = (double *)malloc(sizeof(double) * (size_t)(rows > 0 ? rows : 1) * (size_t)(cols > 0 ? cols : 1));
+    lag_mat_trim_both(x, n, maxLag, includeOriginal, rm);
+    for (int r = 0; r < rows; r++)
+        for (int c = 0; c < cols; c++) out_colmajor[(size_t)c * rows + r] = rm[(size_t)r * cols + c];
+    free(rm);
+    return rows;
+}
+
 /* Autoregression.fitModel(ts, maxLag, noIntercept)  Autoregression.scala:38-53
- * (Y = ts(maxLag until n); X = Lag.lagMatTrimBoth(ts, maxLag), Lag.scala:62-99: X(r)(l-1) = ts(r+maxLag-l)) */
+ * (Y = ts(maxLag until n); X = Lag.lagMatTrimBoth(ts, maxLag), Lag.scala:33-49: X(r)(l-1) = ts(r+maxLag-l)) */
 int orc_ar_fit(const double *ts, int n, int maxLag, int noIntercept, double *c_out, double *coef_out) {
     int rows = n - maxLag;
     if (rows < 0) return ARIMA_ST_SERIES_TOO_SHORT;
     double *X = (double *)malloc(sizeof(double) * (size_t)(rows > 0 ? rows : 1) * (size_t)(maxLag > 0 ? maxLag : 1));
-    for (int r = 0; r < rows; r++)
-        for (int l = 1; l <= maxLag; l++) X[(size_t)r * maxLag + (l - 1)] = ts[r + maxLag - l];
+    lag_mat_trim_both(ts, n, maxLag, 0, X);
     double beta[ORC_KMAX];
     int st = orc_ols(ts + maxLag, X, rows, maxLag, !noIntercept, beta);
     free(X);
@@ -655,6 +675,18 @@ int orc_fit_trace(const double *ts, int T, int p, int d, int q, int I, int smear
     *tr_len = c.tr_len;
     free(tmp);
     return st;
+}
+
+/* Thread count of the batch wrapper (bench.py's CPU baseline times it on the lease's share and on one core). */
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+void orc_set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+#else
+    (void)n;
+#endif
 }
 
 /* Batch wrapper (OpenMP over series when compiled with -fopenmp): the CPU baseline leg of bench.py. */

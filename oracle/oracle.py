@@ -67,8 +67,27 @@ def lib():
                                                      ctypes.c_int, ctypes.c_int, _dp, _dp]
         L.orc_remove_time_dependent_effects.argtypes = [_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                         ctypes.c_int, ctypes.c_int, _dp, _dp]
+        L.orc_lag_matrix.restype = ctypes.c_int
+        L.orc_lag_matrix.argtypes = [_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp]
+        L.orc_set_threads.restype = None
+        L.orc_set_threads.argtypes = [ctypes.c_int]
         _lib = L
     return _lib
+
+
+def lag_matrix(x, max_lag, include_original):
+    """UnivariateTimeSeries.lag / Lag.lagMatTrimBoth (Lag.scala:33-99): (rows, cols, column-major values) -- the
+    layout Matrices.dense(rows, cols, values) takes, and the design the AR / Hannan-Rissanen regressions use."""
+    x, px = _c(x)
+    cols = max_lag + (1 if include_original else 0)
+    out = np.zeros(max(1, (len(x) - max_lag) * cols))
+    rows = lib().orc_lag_matrix(px, len(x), max_lag, int(include_original), out.ctypes.data_as(_dp))
+    return rows, cols, out[: rows * cols]
+
+
+def set_threads(n):
+    """OpenMP threads of fit_batch (bench.py's CPU baseline: the lease's share, then one core)."""
+    lib().orc_set_threads(int(n))
 
 
 def _c(a):

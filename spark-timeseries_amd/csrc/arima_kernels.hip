@@ -334,10 +334,13 @@ __global__ __launch_bounds__(256) void k_search_select(const double *__restrict_
                                                        const double *__restrict__ cand_ll,
                                                        const int32_t *__restrict__ cand_status,
                                                        const uint8_t *__restrict__ cand_flags, int64_t N, int p,
-                                                       int d, int q, int I, double *__restrict__ best_aic,
+                                                       int d, int q, int I,
+                                                       const unsigned long long *__restrict__ fit_ctl,
+                                                       double *__restrict__ best_aic,
                                                        int32_t *__restrict__ order, double *__restrict__ coef) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
+    if (fit_ctl && fit_ctl[26] != 0) return;     // the fit kernel dropped series (watchdog): no candidate is valid
     if (cand_status[i] != ARIMA_ST_OK) return;
     if ((cand_flags[i] & (ARIMA_FLAG_STATIONARY | ARIMA_FLAG_INVERTIBLE)) !=
         (ARIMA_FLAG_STATIONARY | ARIMA_FLAG_INVERTIBLE))
@@ -361,12 +364,13 @@ int launch_search_init(double *best_aic, int32_t *order, double *coef, int64_t N
 }
 
 int launch_search_select(const double *cand_coef, const double *cand_ll, const int32_t *cand_status,
-                         const uint8_t *cand_flags, int64_t N, int p, int d, int q, int I, double *best_aic,
-                         int32_t *order, double *coef, hipStream_t s) {
+                         const uint8_t *cand_flags, int64_t N, int p, int d, int q, int I,
+                         const unsigned long long *fit_ctl, double *best_aic, int32_t *order, double *coef,
+                         hipStream_t s) {
     if (N == 0) return ARIMA_OK;
     if (I + p + q > kSearchK) return ARIMA_E_UNSUPPORTED;
     hipLaunchKernelGGL(k_search_select, dim3(grid_for(N, 256)), dim3(256), 0, s, cand_coef, cand_ll, cand_status,
-                       cand_flags, N, p, d, q, I, best_aic, order, coef);
+                       cand_flags, N, p, d, q, I, fit_ctl, best_aic, order, coef);
     STS_CHECK_LAUNCH();
     return ARIMA_OK;
 }

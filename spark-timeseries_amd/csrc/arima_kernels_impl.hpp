@@ -272,6 +272,14 @@ __device__ __forceinline__ void wave_sync_lds() {
 // accepts an entry only when both its ready word and its tag carry its ticket.
 constexpr int kExpressTagWord = kExpressEntryBytes / 8 - 1;
 
+// ring entries this launch may fill: ctl[19] when the host set it (option "express_ring", tests reach the cap with a
+// small ring), else the whole ring. Tickets beyond it are never filled (their groups retire); their series stay on
+// the bulk path, so reaching the cap changes where a series is fitted, never its result.
+__device__ __forceinline__ unsigned long long express_ring_entries(const unsigned long long *ctl) {
+    const unsigned long long r = ctl[19];
+    return (r == 0 || r > (unsigned long long)kExpressRing) ? (unsigned long long)kExpressRing : r;
+}
+
 // Every word shared between workgroups of a launch is accessed as a GLOBAL (address space 1) agent-scope access,
 // never flat (a flat load can keep hitting this CU's stale L1 line; cdna_hip_programming.md Guideline 16).
 typedef __attribute__((address_space(1))) unsigned long long gu64;
@@ -384,17 +392,18 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
         tk_time = __builtin_amdgcn_s_memrealtime();
     }
     ticket = __shfl(ticket, grp * GL);
+    const unsigned long long xring = express_ring_entries(ctl);
     for (;;) {
         // ---- groups waiting on a ticket: poll (group leader), then load the entry (whole group) ----
         int arrived = 0;
         if (gstate == 0 && glead) {
-            const unsigned e = (unsigned)(ticket % kExpressRing);
+            const unsigned e = (unsigned)(ticket % xring);
             const unsigned long long *ent = reinterpret_cast<const unsigned long long *>(xq + (size_t)e * kExpressEntryBytes);
             // poll the ready word; every 32nd poll reads it at the memory side
             unsigned r = (tk_polls & 31u) == 31u ? rd_fresh(&xready[e]) : ld_agent(&xready[e]);
             if (tk_polls++ == 0) tk_rfirst = r;
             tk_rmax = r > tk_rmax ? r : tk_rmax;
-            if (ticket >= (unsigned long long)kExpressRing) {
+            if (ticket >= xring) {
                 arrived = 2;                                // beyond the ring: never filled
             } else if (r == (unsigned)(ticket + 1)) {
                 arrived = rd_fresh(&ent[kExpressTagWord]) == ticket + 1 ? 1 : 0;
@@ -436,7 +445,7 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
         if (arrived == 2) gstate = 2;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (arrived == 1) {
-            const unsigned e = (unsigned)(ticket % kExpressRing);
+            const unsigned e = (unsigned)(ticket % xring);
             const unsigned long long *src = reinterpret_cast<const unsigned long long *>(xq + (size_t)e * kExpressEntryBytes);
             constexpr int W = (int)(sizeof(FitSlotCore<K>) / 8);
             for (int w = gl; w < W; w += GL) reinterpret_cast<unsigned long long *>(&ES)[w] = rd_fresh(&src[w]);
@@ -562,6 +571,7 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     FitSlot<K> *ws = slots[wave];
+    const unsigned long long xring = express_ring_entries(ctl);
     unsigned long long lane_f = 0, lane_g = 0, wave_f = 0, wave_g = 0, wave_m = 0, evals = 0, grads = 0, hits = 0,
                        chains = 0, rides = 0;
     unsigned round_no = 0;
@@ -783,14 +793,17 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
         refill(my, need);
         if (has_express) {
             // an express wave is waiting: hand it this wave's oldest slot (the likely critical path)
-            unsigned long long wants = 0, filled = 0;
+            unsigned long long wants = 0, filled = 0, fault = 0;
             if (lane0) {
                 wants = ld_agent(&ctl[20]);
                 filled = ld_agent(&ctl[21]);
+                fault = ld_agent(&ctl[26]);
             }
             wants = __shfl(wants, 0);
             filled = __shfl(filled, 0);
-            if (wants > filled && filled < (unsigned long long)kExpressRing) {
+            fault = __shfl(fault, 0);
+            // no donation once a fault is recorded (a retired ticket holder would never write it back)
+            if (wants > filled && filled < xring && fault == 0) {
                 const int donate_min = __any(drained) ? kDonateEvalsDrained : kDonateEvals;
                 unsigned long long key = 0;
 #pragma unroll
@@ -813,7 +826,7 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
                 int claimed = 0;
                 if (lane0 && key) {
                     unsigned long long f = filled;
-                    while (f < wants && f < (unsigned long long)kExpressRing) {
+                    while (f < wants && f < xring) {
                         const unsigned long long prev = cas_agent(&ctl[21], f, f + 1ull);
                         if (prev == f) {
                             jx = f;
@@ -828,7 +841,7 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
                 jx = __shfl(jx, 0);
                 if (claimed) {
                     const int bs = (int)(key & 0xffffull) - 1;
-                    const unsigned e = (unsigned)(jx % kExpressRing);
+                    const unsigned e = (unsigned)(jx % xring);
 #ifdef STS_TIMING
                     if (lane == (bs & 63)) ws[bs].c.t_donate = (double)__builtin_amdgcn_s_memrealtime();
                     wave_sync_lds();

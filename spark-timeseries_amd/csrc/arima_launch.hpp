@@ -10,8 +10,9 @@ int launch_difference(const double *in, int64_t ld_in, double *out, int64_t ld_o
                       int drop, hipStream_t s);
 int launch_search_init(double *best_aic, int32_t *order, double *coef, int64_t N, hipStream_t s);
 int launch_search_select(const double *cand_coef, const double *cand_ll, const int32_t *cand_status,
-                         const uint8_t *cand_flags, int64_t N, int p, int d, int q, int I, double *best_aic,
-                         int32_t *order, double *coef, hipStream_t s);
+                         const uint8_t *cand_flags, int64_t N, int p, int d, int q, int I,
+                         const unsigned long long *fit_ctl, double *best_aic, int32_t *order, double *coef,
+                         hipStream_t s);
 int launch_forecast(const double *ts, int64_t ld_in, const double *coef, int k, double *out, int64_t ld_out,
                     int64_t N, int T, int p, int d, int q, int I, int n_future, hipStream_t s);
 int launch_inverse_difference(const double *in, int64_t ld_in, double *out, int64_t ld_out, int64_t N, int T,

@@ -13,6 +13,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/sparkts_arima.h"
 #include "arima_launch.hpp"
@@ -75,6 +76,18 @@ struct SearchLane {
     DevBuf coef, ll, status, neval, ngrad, flags;
 };
 
+// A device fit larger than one slice (option "fit_slice_bytes" of differenced workspace, default 8 GiB = 1M series of
+// T = 1024) runs as consecutive slices over the fit contexts: the workspaces stay bounded whatever the batch (C3's 8M
+// series on one GPU), and the slices pipeline like consecutive calls. Every slice takes the next slot of a ring with
+// its own timing events and its own pinned copy of the kernel counters, so the call's stats cover every slice. A
+// slot is reused only once its previous slice's copy has landed (host check on its last event).
+constexpr int kSliceSlots = 64;
+struct SliceSlot {
+    hipEvent_t ev[5] = {};                 // start, after differencing, after init, after fit, after the counter copy
+    bool used = false;
+    PendingStats ps;
+};
+
 constexpr int kMaxSearchLanes = 8;
 constexpr int kMaxD = 16;
 constexpr int kMaxPipeline = 4;
@@ -115,12 +128,19 @@ struct arima_handle {
     int smear = 1;           // Breeze 0.12 overlap semantics at ARIMA.scala:526: element-wise copy
     int grid_blocks_override = 0;
     int express_blocks = -1;       // k_cg_fit express workgroups (-1: num_cus / 16)
+    int express_ring = 0;          // express hand-offs per launch (0: the whole ring, sts::kExpressRingEntries)
     int64_t last_express = 0;
     int64_t last_grid = 0;
     int search_lanes = 8;          // concurrent fits of the order search (2/4/8: 1269/1303/1408 series/s, profiles/r02/g_c5)
     int pipeline = 1;              // fit contexts in rotation (option "fit_pipeline")
     int host_pipeline = 3;         // contexts the chunked host path rotates over
     int64_t host_chunk = 1 << 18;  // series per chunk of the host path (option "host_chunk")
+    int64_t fit_slice_bytes = 8ll << 30;   // differenced workspace of one device-fit slice (option "fit_slice_bytes")
+    SliceSlot slot[kSliceSlots];
+    unsigned long long *slot_ctl = nullptr;     // pinned, kCtlWords per slot
+    unsigned slot_seq = 0;                      // slots taken so far
+    unsigned slice_first = 0, slice_n = 0;      // slots of the last sliced fit call (stats_ctx == -2)
+    DevBuf dev_fault;                           // sticky device record of the first fit-kernel fault (6 words)
     unsigned fit_seq = 0;          // fit calls so far (selects the context)
     int stats_ctx = -1;            // context of the last fit (arima_get_last_stats), -1: none
     arima_fit_stats host_acc{};    // host path: counters summed over its chunks
@@ -172,6 +192,13 @@ __global__ void k_fill_status(int64_t N, int k, const int32_t *__restrict__ prio
     if (n_eval_out) n_eval_out[i] = 0;
     if (n_grad_out) n_grad_out[i] = 0;
     if (flags_out) flags_out[i] = 0;
+}
+
+// the first watchdog fault of a fit kernel (its ctl[26..31]) into the handle's sticky device record
+__global__ void k_fault_merge(const unsigned long long *__restrict__ ctl, unsigned long long *__restrict__ rec) {
+    if (threadIdx.x != 0 || ctl[26] == 0) return;
+    if (atomicCAS(&rec[0], 0ull, ctl[26]) == 0ull)
+        for (int i = 1; i < 6; ++i) rec[i] = ctl[26 + i];
 }
 
 int check_orders(arima_handle *h, int p, int d, int q, int I) {
@@ -230,6 +257,11 @@ int arima_create(int device, arima_handle **out) {
         if (rc == ARIMA_OK && hipHostMalloc((void **)&c.ctl_host, kCtlWords * sizeof(unsigned long long), 0) != hipSuccess)
             rc = ARIMA_E_OOM;
     }
+    if (rc == ARIMA_OK &&
+        hipHostMalloc((void **)&h->slot_ctl, (size_t)kSliceSlots * kCtlWords * sizeof(unsigned long long), 0) != hipSuccess)
+        rc = ARIMA_E_OOM;
+    if (rc == ARIMA_OK && h->dev_fault.ensure(8 * sizeof(unsigned long long)) != ARIMA_OK) rc = ARIMA_E_OOM;
+    if (rc == ARIMA_OK && hipMemset(h->dev_fault.ptr, 0, 8 * sizeof(unsigned long long)) != hipSuccess) rc = ARIMA_E_DEVICE;
     if (rc != ARIMA_OK) {
         arima_destroy(h);
         return rc;
@@ -264,6 +296,10 @@ int arima_destroy(arima_handle *h) {
     }
     for (auto &e : h->ev_diff)
         if (e) hipEventDestroy(e);
+    for (auto &sl : h->slot)
+        for (auto &e : sl.ev)
+            if (e) hipEventDestroy(e);
+    if (h->slot_ctl) hipHostFree(h->slot_ctl);
     for (auto &e : h->ev)
         if (e) hipEventDestroy(e);
     if (h->ev_done) hipEventDestroy(h->ev_done);
@@ -275,6 +311,8 @@ int arima_destroy(arima_handle *h) {
 const char *arima_last_error(const arima_handle *h) { return h ? h->err.c_str() : "null handle"; }
 
 static void finish_stats(arima_handle *h, FitCtx &c);
+static arima_fit_stats compute_stats(const PendingStats &ps, const unsigned long long *cc, const hipEvent_t *ev);
+static void acc_stats(arima_fit_stats &a, const arima_fit_stats &s);
 
 int arima_get_last_stats(const arima_handle *hc, arima_fit_stats *out) {
     if (!hc || !out) return ARIMA_E_INVALID_ARG;
@@ -285,6 +323,17 @@ int arima_get_last_stats(const arima_handle *hc, arima_fit_stats *out) {
         hipSetDevice(h->device);
         if (hipEventSynchronize(c.ev_done) != hipSuccess) return set_err(h, ARIMA_E_DEVICE, "stats: device error");
         finish_stats(h, c);
+    } else if (h->stats_ctx == -2 && h->slice_n > 0) {   // a sliced fit: the sum over its slices
+        hipSetDevice(h->device);
+        arima_fit_stats acc{};
+        for (unsigned j = 0; j < h->slice_n; ++j) {
+            const unsigned sl = (h->slice_first + j) % kSliceSlots;
+            SliceSlot &ss = h->slot[sl];
+            if (hipEventSynchronize(ss.ev[4]) != hipSuccess) return set_err(h, ARIMA_E_DEVICE, "stats: device error");
+            acc_stats(acc, compute_stats(ss.ps, h->slot_ctl + (size_t)sl * kCtlWords, ss.ev));
+        }
+        h->stats = acc;
+        h->slice_n = 0;
     }
     *out = h->stats;
     return ARIMA_OK;
@@ -302,6 +351,8 @@ static int check_fault(arima_handle *h, FitCtx &c) {
     return ARIMA_OK;
 }
 
+static int take_fault(arima_handle *h);
+
 int arima_synchronize(arima_handle *h) {
     if (!h) return ARIMA_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
@@ -312,6 +363,12 @@ int arima_synchronize(arima_handle *h) {
         if (c.has_done) HIPCHK(h, hipEventSynchronize(c.ev_done));
         if (rc == ARIMA_OK) rc = check_fault(h, c);
     }
+    for (auto &l : h->lanes)
+        if (l.stream) HIPCHK(h, hipStreamSynchronize(l.stream));
+    // the sticky record every fit kernel's counters are merged into (sliced fits, order-search lanes, contexts whose
+    // pinned counters a later call has already overwritten)
+    const int rf = take_fault(h);
+    if (rc == ARIMA_OK) rc = rf;
     return rc;
 }
 
@@ -319,6 +376,10 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
     if (!h || !name) return ARIMA_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
     if (!strcmp(name, "smear")) { h->smear = value ? 1 : 0; return ARIMA_OK; }
+    if (!strcmp(name, "express_ring")) {
+        h->express_ring = (int)std::min<int64_t>(sts::kExpressRingEntries, std::max<int64_t>(0, value));
+        return ARIMA_OK;
+    }
     if (!strcmp(name, "express_blocks")) { h->express_blocks = (int)std::max<int64_t>(-1, value); return ARIMA_OK; }
     if (!strcmp(name, "grid_blocks")) { h->grid_blocks_override = (int)std::max<int64_t>(0, value); return ARIMA_OK; }
     if (!strcmp(name, "search_lanes")) {
@@ -334,6 +395,7 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
         return ARIMA_OK;
     }
     if (!strcmp(name, "host_chunk")) { h->host_chunk = std::max<int64_t>(1, value); return ARIMA_OK; }
+    if (!strcmp(name, "fit_slice_bytes")) { h->fit_slice_bytes = std::max<int64_t>(1, value); return ARIMA_OK; }
     return set_err(h, ARIMA_E_INVALID_ARG, "unknown option");
 }
 
@@ -379,6 +441,8 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
     RCCHK(h, ws.ctl.ensure(kCtlWords * sizeof(unsigned long long)), "workspace");
     HIPCHK(h, hipMemsetAsync(ws.ctl.ptr, 0, kCtlWords * sizeof(unsigned long long), s));
     HIPCHK(h, hipMemsetAsync(ws.ctl.as<unsigned long long>() + 15, 0xff, sizeof(unsigned long long), s));
+    if (h->express_ring > 0)                                   // ctl[19]: the launch's ring entries (low word)
+        HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)(ws.ctl.as<unsigned long long>() + 19), h->express_ring, 1, s));
     if (p > 0 && q == 0) {                                     // AR-only shortcut, method never checked
         if (ev_mid) HIPCHK(h, hipEventRecord(ev_mid, s));
         RCCHK(h, sts::launch_ar_fit(y, ldn, n, N, p, I, d_coef, d_ll, d_status, d_neval, d_ngrad, d_flags, s),
@@ -428,6 +492,9 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
                                 d_ngrad, d_flags, ws.ctl.as<unsigned long long>(), blocks, xblocks,
                                 ws.xring.as<unsigned char>(), ws.xready.as<unsigned>(), shared_gpu ? 0 : 1, s),
           "cg_fit");
+    hipLaunchKernelGGL(k_fault_merge, dim3(1), dim3(64), 0, s, ws.ctl.as<unsigned long long>(),
+                       h->dev_fault.as<unsigned long long>());
+    HIPCHK(h, hipGetLastError());
     return ARIMA_OK;
 }
 
@@ -449,10 +516,13 @@ static int reserve_fit_ws(arima_handle *h, int count, int64_t N, int64_t ldn, in
 // One fit on context c, enqueued on stream s (the caller has ordered s after what the fit depends on).
 // shared_gpu: fits of other contexts may run concurrently, so the fit kernel's drained workgroups exit (making room
 // for the next fit) instead of joining its express pool.
+// slot >= 0: one slice of a sliced call -- timing events and the counter copy go to that slice slot, and the
+// context keeps no pending stats of its own.
 static int fit_device_locked(arima_handle *h, FitCtx &c, int ci, int reserve, const double *d_series, int64_t N,
                              int32_t T, int64_t ld, int32_t p, int32_t d, int32_t q, int32_t I, int32_t method,
                              const double *d_user_init, double *d_coef, double *d_ll, int32_t *d_status,
-                             int32_t *d_neval, int32_t *d_ngrad, uint8_t *d_flags, hipStream_t s, bool shared_gpu) {
+                             int32_t *d_neval, int32_t *d_ngrad, uint8_t *d_flags, hipStream_t s, bool shared_gpu,
+                             int slot = -1) {
     RCCHK(h, check_orders(h, p, d, q, I), "orders");
     if (N < 0 || T < 0 || ld < T) return set_err(h, ARIMA_E_INVALID_ARG, "bad shape");
     if (!d_coef || !d_ll || !d_status) return set_err(h, ARIMA_E_INVALID_ARG, "null output");
@@ -461,23 +531,29 @@ static int fit_device_locked(arima_handle *h, FitCtx &c, int ci, int reserve, co
     const int n = std::max(T - d, 0);
     const int64_t ldn = round_up(std::max(n, 1), 16);
     c.pending = PendingStats{};
-    h->stats = arima_fit_stats{};
-    h->stats_ctx = ci;
+    if (slot < 0) {
+        h->stats = arima_fit_stats{};
+        h->stats_ctx = ci;
+    }
     if (N == 0) return ARIMA_OK;
 
+    SliceSlot *ss = slot >= 0 ? &h->slot[slot] : nullptr;
+    hipEvent_t *ev = ss ? ss->ev : c.ev;
+    unsigned long long *ctl_dst = ss ? h->slot_ctl + (size_t)slot * kCtlWords : c.ctl_host;
     RCCHK(h, reserve_fit_ws(h, reserve, N, ldn, k), "workspace");
-    HIPCHK(h, hipEventRecord(c.ev[0], s));
+    HIPCHK(h, hipEventRecord(ev[0], s));
     RCCHK(h, sts::launch_difference(d_series, ld, c.diff.as<double>(), ldn, N, T, d, 1, s), "difference");
-    HIPCHK(h, hipEventRecord(c.ev[1], s));
+    HIPCHK(h, hipEventRecord(ev[1], s));
     int64_t grid = 0, xblocks = 0;
     RCCHK(h, fit_kernels(h, c.ws, c.diff.as<double>(), ldn, n, N, p, q, I, method, d_user_init, d_coef, d_ll,
-                         d_status, d_neval, d_ngrad, d_flags, s, c.ev[2], &grid, &xblocks, shared_gpu), "fit");
-    HIPCHK(h, hipEventRecord(c.ev[3], s));
+                         d_status, d_neval, d_ngrad, d_flags, s, ev[2], &grid, &xblocks, shared_gpu), "fit");
+    HIPCHK(h, hipEventRecord(ev[3], s));
     h->last_grid = grid;
     h->last_express = xblocks;
-    HIPCHK(h, hipMemcpyAsync(c.ctl_host, c.ws.ctl.ptr, kCtlWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-    c.fit_ctl = true;
-    PendingStats &ps = c.pending;
+    HIPCHK(h, hipMemcpyAsync(ctl_dst, c.ws.ctl.ptr, kCtlWords * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    if (ss) HIPCHK(h, hipEventRecord(ss->ev[4], s));
+    c.fit_ctl = !ss;
+    PendingStats &ps = ss ? ss->ps : c.pending;
     ps.N = N;
     ps.n = n;
     ps.p = p;
@@ -492,22 +568,21 @@ static int fit_device_locked(arima_handle *h, FitCtx &c, int ci, int reserve, co
     return ARIMA_OK;
 }
 
-// Completes the stats of context c's last fit once its device work has finished.
-static void finish_stats(arima_handle *h, FitCtx &c) {
-    const PendingStats &ps = c.pending;
+// The stats of one finished fit (or slice) from its pending shape, its counter copy and its timing events.
+static arima_fit_stats compute_stats(const PendingStats &ps, const unsigned long long *cc, const hipEvent_t *ev) {
     arima_fit_stats st{};
+    if (!ps.valid) return st;
     const int64_t N = ps.N;
     const int n = ps.n, p = ps.p, q = ps.q, I = ps.I, k = I + p + q;
     float ms = 0;
-    hipEventElapsedTime(&ms, c.ev[0], c.ev[1]);
+    hipEventElapsedTime(&ms, ev[0], ev[1]);
     st.ms_difference = ms;
-    hipEventElapsedTime(&ms, c.ev[1], c.ev[2]);
+    hipEventElapsedTime(&ms, ev[1], ev[2]);
     st.ms_hr_init = ms;
-    hipEventElapsedTime(&ms, c.ev[2], c.ev[3]);
+    hipEventElapsedTime(&ms, ev[2], ev[3]);
     st.ms_cg_fit = ms;
-    hipEventElapsedTime(&ms, c.ev[0], c.ev[3]);
+    hipEventElapsedTime(&ms, ev[0], ev[3]);
     st.ms_total = ms;
-    const unsigned long long *cc = c.ctl_host;
     st.f_passes = (int64_t)cc[1];
     st.g_passes = (int64_t)cc[2];
     st.n_eval = (int64_t)cc[5];
@@ -549,7 +624,12 @@ static void finish_stats(arima_handle *h, FitCtx &c) {
     const double G = (double)(st.g_passes - st.ride_passes + st.express_g_passes);
     st.flops = U * S * ff + G * S * fg + (ps.user_init ? 0.0 : whr);
     st.n_series = N;
-    h->stats = st;
+    return st;
+}
+
+// Completes the stats of context c's last fit once its device work has finished.
+static void finish_stats(arima_handle *h, FitCtx &c) {
+    h->stats = compute_stats(c.pending, c.ctl_host, c.ev);
     c.pending.valid = false;
 }
 
@@ -561,16 +641,54 @@ int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_se
     if (!h) return ARIMA_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
     const int P = h->pipeline;
-    const int ci = (int)(h->fit_seq++ % (unsigned)P);
-    FitCtx &c = h->fctx[ci];
-    hipStream_t s = stream ? (hipStream_t)stream : c.stream;
     HIPCHK(h, hipSetDevice(h->device));
-    begin_fit(h, c, s);
-    const int rc = fit_device_locked(h, c, ci, P, d_series, n_series, T, ld, p, d, q, include_intercept, method,
-                                     d_user_init, d_coef_out, d_css_ll_out, d_status_out, d_n_eval_out, d_n_grad_out,
-                                     d_flags_out, s, P > 1);
-    HIPCHK(h, end_fit(c, s));
-    return rc;
+    const int64_t ldn = round_up(std::max(T - d, 1), 16);
+    const int64_t slice = std::max<int64_t>(1024, h->fit_slice_bytes / (ldn * (int64_t)sizeof(double)) / 1024 * 1024);
+    if (n_series <= slice || T < 0 || ld < T || n_series < 0) {
+        const int ci = (int)(h->fit_seq++ % (unsigned)P);
+        FitCtx &c = h->fctx[ci];
+        hipStream_t s = stream ? (hipStream_t)stream : c.stream;
+        begin_fit(h, c, s);
+        const int rc = fit_device_locked(h, c, ci, P, d_series, n_series, T, ld, p, d, q, include_intercept, method,
+                                         d_user_init, d_coef_out, d_css_ll_out, d_status_out, d_n_eval_out,
+                                         d_n_grad_out, d_flags_out, s, P > 1);
+        HIPCHK(h, end_fit(c, s));
+        return rc;
+    }
+    // sliced: slice j of the batch runs on the next fit context (its own outputs' rows), exactly as consecutive calls
+    RCCHK(h, check_orders(h, p, d, q, include_intercept), "orders");
+    if (!d_coef_out || !d_css_ll_out || !d_status_out) return set_err(h, ARIMA_E_INVALID_ARG, "null output");
+    const int k = include_intercept + p + q;
+    const int64_t nslices = (n_series + slice - 1) / slice;
+    h->stats = arima_fit_stats{};
+    h->stats_ctx = -2;
+    h->slice_first = h->slot_seq % kSliceSlots;
+    h->slice_n = 0;
+    for (int64_t j = 0; j < nslices; ++j) {
+        const int sl = (int)(h->slot_seq++ % kSliceSlots);
+        SliceSlot &ss = h->slot[sl];
+        if (!ss.used) {
+            for (auto &e : ss.ev) HIPCHK(h, hipEventCreate(&e));
+            ss.used = true;
+        } else if (hipEventQuery(ss.ev[4]) != hipSuccess) {
+            HIPCHK(h, hipEventSynchronize(ss.ev[4]));       // its previous slice's counter copy must have landed
+        }
+        ss.ps = PendingStats{};
+        const int64_t f = j * slice, ns = std::min(slice, n_series - f);
+        const int ci = (int)(h->fit_seq++ % (unsigned)P);
+        FitCtx &c = h->fctx[ci];
+        hipStream_t s = stream ? (hipStream_t)stream : c.stream;
+        begin_fit(h, c, s);
+        const int rc = fit_device_locked(
+            h, c, ci, P, d_series + f * ld, ns, T, ld, p, d, q, include_intercept, method,
+            d_user_init ? d_user_init + f * k : nullptr, d_coef_out + f * k, d_css_ll_out + f, d_status_out + f,
+            d_n_eval_out ? d_n_eval_out + f : nullptr, d_n_grad_out ? d_n_grad_out + f : nullptr,
+            d_flags_out ? d_flags_out + f : nullptr, s, P > 1, sl);
+        HIPCHK(h, end_fit(c, s));
+        h->slice_n++;
+        if (rc != ARIMA_OK) return rc;
+    }
+    return ARIMA_OK;
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -736,7 +854,8 @@ int arima_fit_batch(arima_handle *h, const double *series, int64_t N, int32_t T,
     }
     h->stats = h->host_acc;
     h->stats_ctx = -1;
-    return rc;
+    const int rf = take_fault(h);          // already reported per chunk when set: clear the sticky record
+    return rc != ARIMA_OK ? rc : rf;
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -946,42 +1065,70 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
     h->stats = arima_fit_stats{};
     if (N == 0) return ARIMA_OK;
     HIPCHK(h, hipSetDevice(h->device));
-    const int L = h->search_lanes;
-    for (int j = 0; j < L; ++j) {
+    // Differenced copies: one per d, all computed up front, so the lanes run through the d boundaries without
+    // draining -- when they fit in HBM next to the lanes' workspaces; otherwise one shared copy, rewritten for each
+    // d once every fit of the previous d has finished (max_d up to 16 would not fit).
+    size_t diff_bytes = 0;
+    for (int d = 0; d <= max_d; ++d) diff_bytes += (size_t)N * round_up(std::max(T - d, 1), 16) * sizeof(double);
+    const size_t lane_bytes = (size_t)N * (11 * 8 * 2 + 8 + 4 * 4 + 1) + sts::kExpressRingBytes + sts::kExpressReadyBytes;
+    size_t free_b = 0, total_b = 0;
+    HIPCHK(h, hipMemGetInfo(&free_b, &total_b));
+    size_t held = 0;                               // what this handle's search workspaces already hold
+    for (int d = 0; d <= kMaxD; ++d) held += h->os_diff[d].bytes;
+    const bool per_d = diff_bytes + (size_t)h->search_lanes * lane_bytes <= (free_b + held) / 10 * 9;
+    // Lanes: as many of the configured as their workspaces allow (at least one)
+    int L = 0;
+    for (int j = 0; j < h->search_lanes; ++j) {
         SearchLane &ln = h->lanes[j];
         if (!ln.stream) {
             HIPCHK(h, hipStreamCreateWithFlags(&ln.stream, hipStreamNonBlocking));
             HIPCHK(h, hipEventCreateWithFlags(&ln.ev_fit, hipEventDisableTiming));
             HIPCHK(h, hipEventCreateWithFlags(&ln.ev_sel, hipEventDisableTiming));
         }
-        RCCHK(h, ln.coef.ensure((size_t)N * 11 * sizeof(double)), "workspace");
-        RCCHK(h, ln.ll.ensure((size_t)N * sizeof(double)), "workspace");
-        RCCHK(h, ln.status.ensure((size_t)N * sizeof(int32_t)), "workspace");
-        RCCHK(h, ln.neval.ensure((size_t)N * sizeof(int32_t)), "workspace");
-        RCCHK(h, ln.ngrad.ensure((size_t)N * sizeof(int32_t)), "workspace");
-        RCCHK(h, ln.flags.ensure((size_t)N), "workspace");
         // every workspace at its largest size before anything is enqueued: a growing DevBuf frees (hipFree
         // synchronises the device) and would serialise the host loop below with the fits already in flight
-        RCCHK(h, ln.ws.init.ensure((size_t)N * 11 * sizeof(double)), "workspace");
-        RCCHK(h, ln.ws.hr_status.ensure((size_t)N * sizeof(int32_t)), "workspace");
-        RCCHK(h, ln.ws.ctl.ensure(kCtlWords * sizeof(unsigned long long)), "workspace");
-        RCCHK(h, ln.ws.xring.ensure(sts::kExpressRingBytes), "workspace");
-        RCCHK(h, ln.ws.xready.ensure(sts::kExpressReadyBytes), "workspace");
+        int rc = ARIMA_OK;
+        for (DevBuf *b : {&ln.coef, &ln.ws.init})
+            if (rc == ARIMA_OK) rc = b->ensure((size_t)N * 11 * sizeof(double));
+        if (rc == ARIMA_OK) rc = ln.ll.ensure((size_t)N * sizeof(double));
+        for (DevBuf *b : {&ln.status, &ln.neval, &ln.ngrad, &ln.ws.hr_status})
+            if (rc == ARIMA_OK) rc = b->ensure((size_t)N * sizeof(int32_t));
+        if (rc == ARIMA_OK) rc = ln.flags.ensure((size_t)N);
+        if (rc == ARIMA_OK) rc = ln.ws.ctl.ensure(kCtlWords * sizeof(unsigned long long));
+        if (rc == ARIMA_OK) rc = ln.ws.xring.ensure(sts::kExpressRingBytes);
+        if (rc == ARIMA_OK) rc = ln.ws.xready.ensure(sts::kExpressReadyBytes);
+        if (rc != ARIMA_OK) {
+            if (j == 0) return set_err(h, rc, "order search workspace");
+            break;                                 // fewer lanes instead of failing the call
+        }
+        L = j + 1;
     }
-    for (int d = 0; d <= max_d; ++d)
-        RCCHK(h, h->os_diff[d].ensure((size_t)N * round_up(std::max(T - d, 1), 16) * sizeof(double)), "workspace");
+    if (per_d) {
+        for (int d = 0; d <= max_d; ++d)
+            RCCHK(h, h->os_diff[d].ensure((size_t)N * round_up(std::max(T - d, 1), 16) * sizeof(double)), "workspace");
+    } else {
+        RCCHK(h, h->os_diff[0].ensure((size_t)N * round_up(std::max(T, 1), 16) * sizeof(double)), "workspace");
+    }
     HIPCHK(h, hipEventRecord(h->ev[0], s));
     RCCHK(h, sts::launch_search_init(d_aic, d_order, d_coef, N, s), "search_init");
+    auto diff_into = [&](int d, DevBuf &buf) -> int {
+        const int n = std::max(T - d, 0);
+        const int64_t ldn = round_up(std::max(n, 1), 16);
+        if (!h->ev_diff[d]) HIPCHK(h, hipEventCreateWithFlags(&h->ev_diff[d], hipEventDisableTiming));
+        RCCHK(h, sts::launch_difference(d_series, ld, buf.as<double>(), ldn, N, T, d, 1, s), "difference");
+        HIPCHK(h, hipEventRecord(h->ev_diff[d], s));
+        return ARIMA_OK;
+    };
+    if (per_d)                                     // differencesOfOrderD once per d (ARIMA.scala:88)
+        for (int d = 0; d <= max_d; ++d) RCCHK(h, diff_into(d, h->os_diff[d]), "difference");
     const int i_lo = intercept_mode == 1 ? 1 : 0, i_hi = intercept_mode == 0 ? 0 : 1;
     int64_t fits = 0;
     for (int d = 0; d <= max_d; ++d) {
-        // differencesOfOrderD once per d (ARIMA.scala:88), shared read-only by that d's fits on every lane
         const int n = std::max(T - d, 0);
         const int64_t ldn = round_up(std::max(n, 1), 16);
-        RCCHK(h, h->os_diff[d].ensure((size_t)N * ldn * sizeof(double)), "workspace");
-        if (!h->ev_diff[d]) HIPCHK(h, hipEventCreateWithFlags(&h->ev_diff[d], hipEventDisableTiming));
-        RCCHK(h, sts::launch_difference(d_series, ld, h->os_diff[d].as<double>(), ldn, N, T, d, 1, s), "difference");
-        HIPCHK(h, hipEventRecord(h->ev_diff[d], s));
+        DevBuf &dbuf = per_d ? h->os_diff[d] : h->os_diff[0];
+        // shared copy: s has already waited (through the selects) for every fit of d - 1, the copy's readers
+        if (!per_d) RCCHK(h, diff_into(d, dbuf), "difference");
         for (int p = 0; p <= max_p; ++p)
             for (int q = 0; q <= max_q; ++q)
                 for (int I = i_lo; I <= i_hi; ++I) {
@@ -991,16 +1138,18 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
                     HIPCHK(h, hipStreamWaitEvent(ln.stream, h->ev_diff[d], 0));
                     if (ln.sel_recorded) HIPCHK(h, hipStreamWaitEvent(ln.stream, ln.ev_sel, 0));  // outputs read
                     int64_t grid = 0, xb = 0;
-                    RCCHK(h, fit_kernels(h, ln.ws, h->os_diff[d].as<double>(), ldn, n, N, p, q, I, method, nullptr,
+                    RCCHK(h, fit_kernels(h, ln.ws, dbuf.as<double>(), ldn, n, N, p, q, I, method, nullptr,
                                          ln.coef.as<double>(), ln.ll.as<double>(), ln.status.as<int32_t>(),
                                          ln.neval.as<int32_t>(), ln.ngrad.as<int32_t>(), ln.flags.as<uint8_t>(),
                                          ln.stream, nullptr, &grid, &xb, L > 1), "fit");
                     HIPCHK(h, hipEventRecord(ln.ev_fit, ln.stream));
-                    // candidates are merged in grid order on the call's stream (first minimum wins, as minBy)
+                    // candidates are merged in grid order on the call's stream (first minimum wins, as minBy); a
+                    // fit whose kernel recorded a watchdog fault contributes nothing (its outputs are incomplete)
+                    // and the fault reaches the caller through the handle's sticky record (arima_synchronize)
                     HIPCHK(h, hipStreamWaitEvent(s, ln.ev_fit, 0));
                     RCCHK(h, sts::launch_search_select(ln.coef.as<double>(), ln.ll.as<double>(),
                                                        ln.status.as<int32_t>(), ln.flags.as<uint8_t>(), N, p, d, q, I,
-                                                       d_aic, d_order, d_coef, s),
+                                                       ln.ws.ctl.as<unsigned long long>(), d_aic, d_order, d_coef, s),
                           "search_select");
                     HIPCHK(h, hipEventRecord(ln.ev_sel, s));
                     ln.sel_recorded = true;
@@ -1010,6 +1159,28 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
     HIPCHK(h, hipEventRecord(h->ev[3], s));
     if (n_fits) *n_fits = fits;
     return ARIMA_OK;
+}
+
+// The call's stream waits for everything its lanes have been given (also after an error part-way through the grid,
+// ADVICE r2): later calls then wait for the lanes' reads of the search workspaces through h->ev_done.
+static void join_lanes(arima_handle *h, hipStream_t s) {
+    for (auto &ln : h->lanes) {
+        if (!ln.stream) continue;
+        if (hipEventRecord(ln.ev_fit, ln.stream) == hipSuccess) hipStreamWaitEvent(s, ln.ev_fit, 0);
+    }
+}
+
+// Blocking entry points: the fault record covers the lanes' fit kernels (a dropped series must not
+// pass as a candidate, and the call reports ARIMA_E_DEVICE).
+static int take_fault(arima_handle *h) {
+    unsigned long long f[6] = {};
+    HIPCHK(h, hipMemcpy(f, h->dev_fault.ptr, sizeof f, hipMemcpyDeviceToHost));
+    if (f[0] == 0) return ARIMA_OK;
+    HIPCHK(h, hipMemset(h->dev_fault.ptr, 0, 8 * sizeof(unsigned long long)));
+    char msg[160];
+    snprintf(msg, sizeof msg, "fit kernel watchdog fault %llu (info %llu %llu %llu %llu %llu)", f[0], f[1], f[2],
+             f[3], f[4], f[5]);
+    return set_err(h, ARIMA_E_DEVICE, msg);
 }
 
 int arima_order_search_batch_device(arima_handle *h, const double *d_series, int64_t n_series, int32_t T,
@@ -1022,9 +1193,9 @@ int arima_order_search_batch_device(arima_handle *h, const double *d_series, int
     begin_call(h, s);
     const int rc = order_search_locked(h, d_series, n_series, T, ld, max_p, max_d, max_q, intercept_mode, method,
                                        d_order_out, d_coef_out, d_aic_out, nullptr, s);
-    if (rc != ARIMA_OK) return rc;
+    join_lanes(h, s);
     HIPCHK(h, end_call(h, s));
-    return ARIMA_OK;
+    return rc;
 }
 
 int arima_order_search_batch(arima_handle *h, const double *series, int64_t N, int32_t T, int32_t max_p,
@@ -1045,13 +1216,16 @@ int arima_order_search_batch(arima_handle *h, const double *series, int64_t N, i
     if (T > 0) HIPCHK(h, hipMemcpyAsync(h->h_series.ptr, series, (size_t)N * T * sizeof(double), hipMemcpyHostToDevice, s));
     int rc = order_search_locked(h, h->h_series.as<double>(), N, T, T, max_p, max_d, max_q, intercept_mode, method,
                                  h->os_order.as<int32_t>(), h->h_aux.as<double>(), h->h_ll.as<double>(), nullptr, s);
-    if (rc != ARIMA_OK) return rc;
-    HIPCHK(h, hipMemcpyAsync(order_out, h->os_order.ptr, (size_t)N * 4 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    HIPCHK(h, hipMemcpyAsync(coef_out, h->h_aux.ptr, (size_t)N * 11 * sizeof(double), hipMemcpyDeviceToHost, s));
-    HIPCHK(h, hipMemcpyAsync(aic_out, h->h_ll.ptr, (size_t)N * sizeof(double), hipMemcpyDeviceToHost, s));
+    join_lanes(h, s);
+    if (rc == ARIMA_OK) {
+        HIPCHK(h, hipMemcpyAsync(order_out, h->os_order.ptr, (size_t)N * 4 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipMemcpyAsync(coef_out, h->h_aux.ptr, (size_t)N * 11 * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipMemcpyAsync(aic_out, h->h_ll.ptr, (size_t)N * sizeof(double), hipMemcpyDeviceToHost, s));
+    }
     HIPCHK(h, end_call(h, s));
     HIPCHK(h, hipStreamSynchronize(s));
-    return ARIMA_OK;
+    if (rc != ARIMA_OK) return rc;
+    return take_fault(h);
 }
 
 int arima_sample_batch_device(arima_handle *h, double *d_series, int64_t N, int32_t T, int64_t ld, int32_t p,

@@ -114,8 +114,16 @@ STS_HD STS_FI bool brent_first_u(double A, double B, double C, double &u) {
     return brent_golden_u(a, b, B, u);
 }
 
-// NS: predicted alphas posted with one F request; NC: values cached per line search.
-template <int K, int NS_, int NC_>
+// Evaluations one CG iteration costs once the point is non-finite: every objective value is then NaN without a pass
+// (PC_EVAL), so the iteration is value-independent -- the top-of-loop F(point), BracketFinder's f(0), f(1e-8) and
+// f(xC) (`fC > fB` is false for NaN: the bracket closes at once on (0, 1e-8, xC)), Brent's f(mid) and its
+// golden-section steps on [0, xC] (every comparison with NaN is false, so x stays at 1e-8 and the parabola is never
+// taken) until the interval is below tolerance. tests/test_cglane_sim.py steps the machine to check the constant.
+constexpr int kNanIterEvals = 77;
+
+// NS: predicted alphas posted with one F request; NC: values cached per line search. FF: fast-forward the
+// NaN-absorbing state in closed form (PC_TOP below); false only in the CPU simulator, to check kNanIterEvals.
+template <int K, int NS_, int NC_, bool FF = true>
 struct CGLane {
     static constexpr int NS = NS_;
     static constexpr int NC = NC_;
@@ -318,6 +326,25 @@ struct CGLane {
                 break;
             }
             case PC_TOP: {
+                if constexpr (FF) {
+                    // NaN-absorbing state: a non-finite coordinate makes every later evaluation
+                    // NaN (point + alpha * dir is never finite), and with F(point) = NaN the convergence test is
+                    // false, so the reference runs kNanIterEvals evaluations per iteration (one gradient each, at the
+                    // end) until MaxEval. Jump there: the m iterations that still fit complete, the next one stops
+                    // inside with MAX_EVAL at n_eval = kMaxEval (iter <= n_eval / 2, so MaxIter cannot come first).
+                    // Failed fits report NaN coefficients, so the point itself no longer matters.
+                    bool pfin = true;
+#pragma unroll
+                    for (int i = 0; i < K; ++i) pfin = pfin && finite(point[i]);
+                    if (!pfin && __builtin_isnan(memo_obj)) {
+                        const int m = (kMaxEval - (int)n_eval) / kNanIterEvals;
+                        n_grad = (uint16_t)(n_grad + m);
+                        iter = (uint16_t)(iter + m + 1);
+                        n_eval = (uint16_t)kMaxEval;
+                        fail(ARIMA_ST_MAX_EVAL);
+                        return;
+                    }
+                }
                 if (iter + 1 > kMaxIter) { fail(ARIMA_ST_MAX_ITER); return; }
                 iter++;
                 if (n_eval + 1 > kMaxEval) { fail(ARIMA_ST_MAX_EVAL); return; }

@@ -101,6 +101,32 @@ int dispatch_policy(int ns, int nc, const double *y, int64_t N, int ld, int n, i
 
 }  // namespace
 
+// Evaluations per CG iteration of the NaN-absorbing state, counted by stepping the machine WITHOUT the fast-forward
+// (a non-finite point, F(point) = NaN; every request answered with NaN), and the constant the kernel uses for it.
+extern "C" int sim_nan_iter_evals(int dir_finite) {
+    // advance() runs the absorbing state to MaxEval in one call, so E is found as the smallest evaluation budget
+    // x (n_eval = MaxEval - x at the top of the loop) in which one whole iteration -- one gradient -- completes
+    for (int x = 1; x <= 1000; ++x) {
+        sts::CGLane<5, 2, 4, false> L;
+        double x0[5] = {NAN, 0.1, 0.2, 0.3, 0.4};
+        L.start(x0);
+        L.pc = sts::PC_TOP;
+        L.memo_obj = NAN;
+        L.prev_obj = NAN;
+        L.have_prev_obj = 1;
+        for (int i = 0; i < 5; ++i) L.dir[i] = dir_finite ? 1.0 : NAN;
+        L.n_eval = (uint16_t)(sts::kMaxEval - x);
+        L.n_grad = 0;
+        const double g[5] = {NAN, NAN, NAN, NAN, NAN};
+        L.advance(NAN, g);
+        if (!L.done() || L.status != ARIMA_ST_MAX_EVAL || L.n_eval != sts::kMaxEval) return -1;  // never a pass
+        if (L.n_grad == 1) return x;
+    }
+    return -2;
+}
+
+extern "C" int sim_k_nan_iter_evals() { return sts::kNanIterEvals; }
+
 // Fits N already-differenced series (row i at y + i * ld, length n) from the given initial points (N x K).
 // counts (N x 14): n_eval, n_grad, F passes, G passes, speculative hits, objective chains evaluated, then F passes by resume point (FB, FC, SHIFT_EV, A1, C1, Brent u1, Brent later, other).
 extern "C" int sim_fit_batch(const double *y, int64_t N, int ld, int n, int p, int q, int I, int smear,

@@ -65,3 +65,9 @@ def sim_fit(series, p, d, q, I, smear=O.DEFAULT_SMEAR, ns=1, nc=1):
         coef[idx], ll[idx], status[idx], counts[idx] = c, l, s, cn
     return dict(status=status, coef=coef, ll=ll, n_eval=counts[:, 0], n_grad=counts[:, 1], passes_f=counts[:, 2],
                 passes_g=counts[:, 3], spec_hits=counts[:, 4], chains=counts[:, 5], f_by_phase=counts[:, 6:])
+
+
+def nan_iter_evals(dir_finite=True):
+    """Evaluations per CG iteration in the NaN-absorbing state, stepped (no fast-forward), and the kernel's constant."""
+    L = lib()
+    return L.sim_nan_iter_evals(int(dir_finite)), L.sim_k_nan_iter_evals()

@@ -58,3 +58,25 @@ def test_speculation_saves_passes():
     pb = (base["passes_f"] + base["passes_g"]).sum()
     ps = (spec["passes_f"] + spec["passes_g"]).sum()
     assert ps < 0.75 * pb, (ps, pb)
+
+
+@pytest.mark.parametrize("dir_finite", [True, False])
+def test_nan_fast_forward_constant(dir_finite):
+    # cg_lane.hpp jumps the NaN-absorbing state (non-finite point, NaN objective) to MaxEval in closed form with
+    # kNanIterEvals evaluations per iteration; stepping the same machine without the jump must agree
+    stepped, const = S.nan_iter_evals(dir_finite)
+    assert stepped == const, (stepped, const)
+
+
+def test_fast_forward_matches_oracle_on_c4_fixture():
+    # C4's model (ARIMA(5,1,5)+c, T = 512): most fits end at MaxEval after the point turns non-finite; the fast-forward
+    # must leave status, n_eval, n_grad and the converged fits' results exactly as the oracle steps them
+    meta, arr = load_case("c4_515_T512")
+    s = arr["series"]
+    r = S.sim_fit(s, 5, 1, 5, 1, ns=2, nc=4)
+    ok = r["status"] >= 0
+    assert np.array_equal(r["status"][ok], arr["status"][ok])
+    assert (r["status"][ok] == 1).sum() > 0                     # MAX_EVAL fits are in the fixture
+    assert np.array_equal(r["n_eval"][ok], arr["n_eval"][ok]) and np.array_equal(r["n_grad"][ok], arr["n_grad"][ok])
+    conv = ok & (r["status"] == 0)
+    assert np.array_equal(r["coef"][conv], arr["coef"][conv]) and np.array_equal(r["ll"][conv], arr["ll"][conv])

@@ -529,3 +529,63 @@ def test_wire_format_partition_fit_matches_oracle(engine):
     assert [k for k, _ in out] == [f"s{i}" for i in range(40)]
     for k, c in out:
         assert _same(c, exp[k]), k
+
+
+@pytest.mark.parametrize("pipeline", [1, 3])
+def test_sliced_device_fit_matches_unsliced(engine, pipeline):
+    # arima_fit_batch_device over more series than one slice (option fit_slice_bytes: 1024 series of T = 1024 here)
+    # runs slice by slice over the fit contexts -- the path that bounds C3's 8M-series workspaces on one GPU. Results
+    # must equal the one-slice fit bit for bit, and the stats must sum over every slice.
+    import torch
+    N, T = 5000, 1024
+    s = _device_sample(engine, N, T, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 4242)
+
+    def run():
+        r = [torch.empty((N, 5), dtype=torch.float64, device=s.device),
+             torch.empty(N, dtype=torch.float64, device=s.device)] + \
+            [torch.empty(N, dtype=torch.int32, device=s.device) for _ in range(3)] + \
+            [torch.empty(N, dtype=torch.uint8, device=s.device)]
+        engine.fit_batch_device(s.data_ptr(), N, T, T, 2, 1, 2, True, *[t.data_ptr() for t in r])
+        return [t.cpu().numpy() for t in r], engine.stats()
+
+    whole, st_whole = run()
+    engine.set_option("fit_slice_bytes", 1024 * 1024 * 8)
+    engine.set_option("fit_pipeline", pipeline)
+    try:
+        sliced, st = run()
+    finally:
+        engine.set_option("fit_slice_bytes", 8 << 30)
+        engine.set_option("fit_pipeline", 1)
+    for x, y in zip(whole, sliced):
+        assert _same(x, y)
+    assert st["n_series"] == N and st["n_eval"] == int(whole[3].sum()) and st["n_grad"] == int(whole[4].sum()), st
+    assert st["n_eval"] == st_whole["n_eval"] and st["ms_cg_fit"] > 0
+
+
+def test_express_ring_cap_is_transparent(engine):
+    # the express hand-off ring holds a fixed number of entries per launch (32768); tickets beyond it are never
+    # filled and their series stay on the bulk path. A 4-entry ring reaches that cap at once on the pressure
+    # workload: results must still equal the express-free run bit for bit.
+    import torch
+    N, T = 1 << 15, 1024
+    s = _device_sample(engine, N, T, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 20261015)
+    outs = {}
+    for xb, ring in ((0, 0), (-1, 4)):
+        engine.set_option("express_blocks", xb)
+        engine.set_option("express_ring", ring)
+        try:
+            r = [torch.empty((N, 6), dtype=torch.float64, device=s.device),
+                 torch.empty(N, dtype=torch.float64, device=s.device)] + \
+                [torch.empty(N, dtype=torch.int32, device=s.device) for _ in range(3)] + \
+                [torch.empty(N, dtype=torch.uint8, device=s.device)]
+            engine.fit_batch_device(s.data_ptr(), N, T, T, 3, 1, 2, True, *[t.data_ptr() for t in r])
+            st = engine.stats()
+        finally:
+            engine.set_option("express_blocks", -1)
+            engine.set_option("express_ring", 0)
+        outs[ring] = ([t.cpu().numpy() for t in r], st)
+    (a, _), (b, st) = outs[0], outs[4]
+    assert 0 < st["express_series"] <= 4, st
+    assert st["fault"] == 0
+    for x, y in zip(a, b):
+        assert _same(x, y)

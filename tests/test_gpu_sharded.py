@@ -1,0 +1,52 @@
+"""The series-sharded path on the GPU (the unit it replaces is TimeSeriesRDD.mapSeries,
+TimeSeriesRDD.scala:249-251): two ranks launched by torch.distributed.run -- a launcher process that never touches
+the GPU -- each fit their contiguous shard of the same C2 batch on GPU 0 (device override) through the C ABI; the
+results gathered on rank 0 must equal a single-rank fit of the whole batch bit for bit."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(world, out, total):
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join([os.path.join(ROOT, "spark-timeseries_amd"),
+                                                       os.environ.get("PYTHONPATH", "")]),
+               HSA_ENABLE_IPC_MODE_LEGACY="0", SPARKTS_DEVICE="0")
+    args = ["-m", "sparkts_amd.shard_fit", "--total", str(total), "--T", "1024", "--out", out]
+    if world == 1:
+        cmd = [sys.executable] + args
+    else:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + args
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    z = np.load(out, allow_pickle=False)
+    return json.loads(str(z["meta"])), {k: z[k] for k in z.files if k != "meta"}
+
+
+def test_two_ranks_on_one_gpu_match_single_rank(tmp_path):
+    total = 40000                              # odd split: shards of 20000 / 20000 -> also try a ragged total
+    m1, one = _run(1, str(tmp_path / "one.npz"), total + 1)
+    m2, two = _run(2, str(tmp_path / "two.npz"), total + 1)
+    assert m1["world"] == 1 and m2["world"] == 2
+    for k in one:
+        a, b = one[k], two[k]
+        assert a.shape == b.shape, k
+        assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), k
+    assert (one["status"] == 0).mean() > 0.99

@@ -107,15 +107,20 @@ def test_differencing_kats():
 
 
 def test_lag_matrix_layout_kat():
-    # UnivariateTimeSeriesSuite.scala:31-39 via the AR design (Lag.lagMatTrimBoth, row r = [x(r+m-1) .. x(r)])
+    # UnivariateTimeSeriesSuite.scala:30-38, exactly: lag([1..5], 2, true) = Matrices.dense(3, 3, [3,4,5,2,3,4,1,2,3])
+    # and lag([1..5], 2, false) = Matrices.dense(3, 2, [2,3,4,1,2,3]) (column-major values)
     x = np.array([1.0, 2.0, 3.0, 4.0, 5.0])
-    # an exact AR(2) fit through the intercept-free OLS recovers x(t) = a1 x(t-1) + a2 x(t-2) on a known recursion
+    rows, cols, v = O.lag_matrix(x, 2, True)
+    assert (rows, cols) == (3, 3) and v.tolist() == [3.0, 4.0, 5.0, 2.0, 3.0, 4.0, 1.0, 2.0, 3.0]
+    rows, cols, v = O.lag_matrix(x, 2, False)
+    assert (rows, cols) == (3, 2) and v.tolist() == [2.0, 3.0, 4.0, 1.0, 2.0, 3.0]
+    # the AR design of Autoregression.fitModel is that matrix (the oracle's AR fit builds it with the same code): an
+    # exact AR(2) recursion is recovered through the intercept-free OLS
     y = [1.0, 2.0]
     for _ in range(10):
         y.append(0.5 * y[-1] + 0.25 * y[-2])
     st, c, a = O.ar_fit(np.array(y), 2, no_intercept=True)
     assert st == 0 and np.allclose(a, [0.5, 0.25], atol=1e-12)
-    assert x.size == 5
 
 
 @pytest.mark.parametrize("coef", [[1.5, 0.2], [1.5, 0.2, 0.3]])

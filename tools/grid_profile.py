@@ -54,6 +54,10 @@ def main():
         stc = torch.bincount(st.long(), minlength=11).cpu().tolist()
         r = dict(order=[p, d, q, I], ms_total=round(x["ms_total"], 2), ms_fit=round(x["ms_cg_fit"], 2),
                  mean_eval=round(float(ne.double().mean()), 1), max_eval=int(ne.max()),
+                 mean_grad=round(float(ng.double().mean()), 2), maxeval_frac=round(stc[1] / N, 4),
+                 passes_per_series=round((x["f_passes"] + x["g_passes"] + x["express_f_passes"] +
+                                          x["express_g_passes"]) / N, 2),
+                 flops=x["flops"], tflops=round(x["flops"] / max(x["ms_total"], 1e-9) / 1e9, 3),
                  express_series=x["express_series"], status={k: v for k, v in enumerate(stc) if v})
         rows.append(r)
         tot_ms += x["ms_total"]

@@ -5,8 +5,10 @@ streaming read on gfx950 (so it is doubled here); WRITE_SIZE is taken as is. SQ_
 SQ_ACTIVE_* count quad-cycles. Values are per launch (counter sum / launches of that kernel in the pass).
 
 usage: python tools/summarize_prof.py gpurun_out [out.txt] [--traffic tools/pmc_traffic_c2.json --source NAME]
-(--traffic writes k_cg_fit's measured HBM bytes per launch for bench.py's roofline.traffic; the workload keys
- are those of bench.py's default C2 run that tools/profile.sh profiles)
+                                     [--workload '{"series": ..., "T": ..., "p": .., "d": .., "q": .., "I": .., "smear": ..}']
+(--traffic adds k_cg_fit's measured HBM bytes per launch, keyed by the workload AND the sha256 of the profiled
+ library spark-timeseries_amd/libsparkts_arima.so, to the record list bench.py reads for roofline.traffic; bench.py
+ reports them only for the same workload and build. Default workload: bench.py's C2 run that tools/profile.sh profiles)
 """
 import csv
 import glob
@@ -56,6 +58,12 @@ def main():
         i = argv.index("--source")
         source = argv[i + 1]
         del argv[i:i + 2]
+    workload = {"series": 1048576, "T": 1024, "p": 2, "d": 1, "q": 2, "I": 1, "smear": 1}
+    if "--workload" in argv:
+        import json
+        i = argv.index("--workload")
+        workload = json.loads(argv[i + 1])
+        del argv[i:i + 2]
     sys.argv = argv
     root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
     ks = kernel_stats(root)
@@ -82,12 +90,16 @@ def main():
                 extra = f"  -> HBM write {b / 1e9:.3f} GB/launch"
             lines.append(f"   {name:28s} {mean:18.1f}{extra}")
     txt = "\n".join(lines)
-    fit = cs.get("k_cg_fit<2, 2, 1, false, 4>") or next((v for k, v in cs.items() if k.startswith("k_cg_fit")), {})
+    fit = next((v for k, v in cs.items() if k.startswith("k_cg_fit")), {})
     if traffic_path and "FETCH_SIZE" in fit and "WRITE_SIZE" in fit:
+        import hashlib
         import json
         rd = sum(fit["FETCH_SIZE"]) / len(fit["FETCH_SIZE"]) * 1024 * 2
         wr = sum(fit["WRITE_SIZE"]) / len(fit["WRITE_SIZE"]) * 1024
-        out = {"workload": {"series": 1048576, "T": 1024, "p": 2, "d": 1, "q": 2, "I": 1, "smear": 1},
+        lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "spark-timeseries_amd",
+                           "libsparkts_arima.so")
+        sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()
+        out = {"workload": workload, "build_sha": sha,
                "kernel": "k_cg_fit", "hbm_bytes_per_launch": rd + wr, "read_bytes": rd, "write_bytes": wr,
                "source": source or root}
 
@@ -100,7 +112,14 @@ def main():
                 out["valu_busy"] = mean("SQ_ACTIVE_INST_VALU") / wc
             if mean("SQ_WAIT_ANY") is not None:
                 out["wait_frac"] = mean("SQ_WAIT_ANY") / wc
-        json.dump(out, open(traffic_path, "w"), indent=1)
+        try:
+            recs = json.load(open(traffic_path))
+            recs = recs if isinstance(recs, list) else [recs]
+        except (OSError, ValueError):
+            recs = []
+        recs = [r for r in recs if not (r.get("workload") == workload and r.get("build_sha") == sha)
+                and r.get("build_sha")] + [out]
+        json.dump(recs, open(traffic_path, "w"), indent=1)
     print(txt)
     if len(sys.argv) > 2:
         open(sys.argv[2], "w").write(txt + "\n")
