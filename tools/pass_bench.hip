@@ -63,6 +63,26 @@ __global__ __launch_bounds__(64 * W) void k_lane(const double *__restrict__ y, i
     out[g] = acc;
 }
 
+// gradient pass (css_pass<..., G = true, smear>), one chain, per lane over its own row
+template <int W>
+__global__ __launch_bounds__(64 * W) void k_lane_g(const double *__restrict__ y, int64_t ld, int n, int rows_per_lane,
+                                                   int passes, double *__restrict__ out) {
+    const int64_t G = (int64_t)gridDim.x * blockDim.x;
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    double acc = 0.0;
+    for (int rr = 0; rr < rows_per_lane; ++rr) {
+        const double *row = y + (g + rr * G) * ld;
+        for (int ps = 0; ps < passes; ++ps) {
+            double c[K_] = {8.2 + 1e-3 * ps, 0.2, 0.5, 0.3, 0.1 + 1e-5 * rr}, css, gr[K_];
+            css_pass<P_, Q_, I_, true, true>(row, n, c, css, gr);
+            acc += css;
+#pragma unroll
+            for (int j = 0; j < K_; ++j) acc += gr[j];
+        }
+    }
+    out[g] = acc;
+}
+
 // ---------------------------------------------------------------------------------------------------------------
 // cooperative variant: LDS ring of R slots per wave, one slot = 64 rows x 16 doubles (8 KB)
 __device__ __forceinline__ void glds16(const void *g, void *lds) {
@@ -215,8 +235,16 @@ int main(int argc, char **argv) {
 #define RUN_GLDS(NCH, W, R, BPC)                                                                         \
     run("glds NCH=" #NCH " W=" #W " R=" #R " blk/CU=" #BPC, k_glds<NCH, W, R>, cus * BPC, 64 * W, y, ld, n, rpl, \
         passes, out, bytes((int64_t)cus * BPC * 64 * W))
+#define RUN_LANEG(W, BPC)                                                                                \
+    run("laneG W=" #W " blk/CU=" #BPC, k_lane_g<W>, cus * BPC, 64 * W, y, ld, n, rpl, passes, out,               \
+        bytes((int64_t)cus * BPC * 64 * W))
+    // waves per SIMD = W * BPC / 4: the issue efficiency of one pass type at 1 / 2 waves per SIMD
     RUN_LANE(1, 4, 1);
     RUN_LANE(1, 4, 2);
+    RUN_LANE(3, 4, 1);
+    RUN_LANE(3, 4, 2);
+    RUN_LANEG(4, 1);
+    RUN_LANEG(4, 2);
     RUN_LANE(2, 4, 1);
     RUN_LANE(4, 4, 1);
     RUN_GLDS(1, 4, 2, 1);
