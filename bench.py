@@ -97,6 +97,11 @@ def physical_cores():
         return None
 
 
+def eng_fit_kernel(eng):
+    """The fit kernel variant the engine runs (option fit_kernel)."""
+    return eng.get_option("fit_kernel")
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -193,6 +198,7 @@ def main():
     ap.add_argument("--pipeline", type=int, default=3)
     ap.add_argument("--express-blocks", type=int, default=-1, help="express workgroups of the fit kernel (-1: CUs/16)")
     ap.add_argument("--e2e", type=int, default=1, choices=[0, 1])
+    ap.add_argument("--fit-kernel", type=int, default=-1, help="0: k_cg_fit (LDS slots), 1: k_cg_fit_g; -1: default")
     ap.add_argument("--device", type=int, default=None, help="GPU of every rank (default: LOCAL_RANK's)")
     ap.add_argument("--dry-run", action="store_true")
     args = ap.parse_args()
@@ -258,6 +264,8 @@ def main():
     eng.set_option("smear", args.smear)
     eng.set_option("fit_pipeline", args.pipeline)
     eng.set_option("express_blocks", args.express_blocks)
+    if args.fit_kernel >= 0:
+        eng.set_option("fit_kernel", args.fit_kernel)
     if args.grid_blocks:
         eng.set_option("grid_blocks", args.grid_blocks)
 
@@ -359,6 +367,8 @@ def main():
                        "series_per_gpu": N, "series_total": total_series, "series_len": T,
                        "parallelism": f"series-sharded x{world}, no collective",
                        "breeze_overlap": "smear" if args.smear else "shift",
+                       "fit_kernel": "k_cg_fit_g (slot records in HBM, 2 waves/SIMD)" if eng_fit_kernel(eng) == 1
+                       else "k_cg_fit (LDS slots, 1 wave/SIMD)",
                        "converged_fraction": conv,
                        "mean_n_eval": s0["n_eval"] / max(N, 1), "mean_n_grad": s0["n_grad"] / max(N, 1),
                        "lane_f_passes_per_series": s0["f_passes"] / max(N, 1),

@@ -113,8 +113,12 @@ int         arima_synchronize(arima_handle *h);
 /* Tuning knobs (not part of the reference contract): "smear" (Breeze reading at ARIMA.scala:526, default 1),
  * "fit_pipeline" (fit contexts in rotation for *_device fits, 1..4, default 1), "host_chunk" / "host_pipeline"
  * (series per chunk and contexts of the chunked host path, default 262144 / 3), "express_blocks",
- * "grid_blocks", "search_lanes" (in-kernel scheduler and order-search concurrency). */
+ * "grid_blocks", "search_lanes" (in-kernel scheduler and order-search concurrency), "fit_kernel" (0: k_cg_fit with
+ * LDS-resident optimizer slots, 1: k_cg_fit_g with slot records in HBM and two waves per SIMD), "fit_slice_bytes"
+ * (differenced workspace of one slice of a large device fit), "express_ring" (express hand-offs per launch). */
 int         arima_set_option(arima_handle *h, const char *name, int64_t value);
+/* Current value of a tuning knob (the names arima_set_option takes); ARIMA_E_INVALID_ARG for an unknown name. */
+int         arima_get_option(const arima_handle *h, const char *name, int64_t *value);
 
 /* ---- ARIMA.fitModel over a batch (ARIMA.scala:79-116) ----------------------------------------------- *
  * series    N x T host, series-major                 user_init  NULL (Hannan-Rissanen, ARIMA.scala:216) or N x k

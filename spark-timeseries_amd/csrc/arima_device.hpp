@@ -167,7 +167,7 @@ constexpr int kPrefetchG = STS_PREFETCH_G;   // ... in gradient passes (5x the V
 
 // Full pass. G = false: objective only -> css. G = true: also gradientlogLikelihoodCSSARMA -> g[] (already
 // divided by -sigma2, :532). SMEAR selects the Breeze overlap semantics of :526 (false = row shift).
-template <int P, int Q, int I, bool G, bool SMEAR>
+template <int P, int Q, int I, bool G, bool SMEAR, int DPF = (G ? kPrefetchG : kPrefetchF)>
 __device__ __forceinline__ void css_pass(const double *__restrict__ row, int n,
                                          const double (&c)[I + P + Q > 0 ? I + P + Q : 1], double &css_out,
                                          double (&g)[I + P + Q > 0 ? I + P + Q : 1]) {
@@ -251,7 +251,7 @@ __device__ __forceinline__ void css_pass(const double *__restrict__ row, int n,
             yl[0] = yi;
         }
     };
-    stream_elems<G ? kPrefetchG : kPrefetchF>(row, M, n, step);
+    stream_elems<DPF>(row, M, n, step);
     css_out = css;
     if constexpr (G) {
 #pragma unroll
@@ -261,7 +261,7 @@ __device__ __forceinline__ void css_pass(const double *__restrict__ row, int n,
 
 // Objective pass for NCH points at once (speculative line-search points): NCH independent recursions over the
 // same streamed series. Each chain is exactly the single-point objective (same ops, same order).
-template <int P, int Q, int I, int NCH>
+template <int P, int Q, int I, int NCH, int DPF = kPrefetchF>
 __device__ __forceinline__ void css_pass_multi(const double *__restrict__ row, int n,
                                                const double (&c)[NCH][I + P + Q > 0 ? I + P + Q : 1],
                                                double (&css_out)[NCH]) {
@@ -295,7 +295,7 @@ __device__ __forceinline__ void css_pass_multi(const double *__restrict__ row, i
             yl[0] = yi;
         }
     };
-    stream_elems<kPrefetchF>(row, M, n, step);
+    stream_elems<DPF>(row, M, n, step);
 #pragma unroll
     for (int h = 0; h < NCH; ++h) css_out[h] = css[h];
 }

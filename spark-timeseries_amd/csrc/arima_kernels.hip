@@ -566,17 +566,18 @@ int launch_cg_fit(const double *y, int64_t ld, int n, int64_t N, int p, int q, i
                   const double *init, const int32_t *init_status, double *coef_out, double *ll_out,
                   int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
                   unsigned long long *ctl, int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready,
-                  int join_express, hipStream_t s) {
+                  int join_express, int variant, unsigned char *slot_mem, hipStream_t s) {
     if (N == 0) return ARIMA_OK;
 #define C_(PP)                                                                                             \
     launch_cg_fit_P<PP>(y, ld, n, N, q, I, smear, init, init_status, coef_out, ll_out, status_out, n_eval_out, \
-                        n_grad_out, flags_out, ctl, grid_blocks, express_blocks, xq, xready, join_express, s)
+                        n_grad_out, flags_out, ctl, grid_blocks, express_blocks, xq, xready, join_express, variant, \
+                        slot_mem, s)
     STS_P_SWITCH(C_)
 #undef C_
 }
 
-int cg_fit_series_per_block(int p, int q, int I) {
-#define C_(PP) cg_fit_series_per_block_P<PP>(q, I)
+int cg_fit_series_per_block(int p, int q, int I, int variant) {
+#define C_(PP) cg_fit_series_per_block_P<PP>(q, I, variant)
     STS_P_SWITCH(C_)
 #undef C_
 }

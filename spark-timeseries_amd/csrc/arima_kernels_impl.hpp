@@ -907,6 +907,12 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
     atomicAdd(&ctl[18], rides);
 }
 
+}  // namespace sts
+
+#include "arima_fit_global.hpp"
+
+namespace sts {
+
 // =======================================================================================================
 // Building blocks at given coefficients
 // =======================================================================================================
@@ -1035,24 +1041,35 @@ int launch_ar_fit_P(const double *y, int64_t ld, int n, int64_t N, int I, double
 }
 
 // k_cg_fit launcher for one AR order and Breeze reading (each instantiated in its own translation unit,
-// arima_cg_p<P>_s<S>.hip, so the build parallelises over the heaviest kernel)
+// arima_cg_p<P>_s<S>.hip, so the build parallelises over the heaviest kernel). variant 0: k_cg_fit (LDS slots, one
+// wave per SIMD); variant 1: k_cg_fit_g (slot records in slot_mem, two waves per SIMD).
 template <int P, bool S>
 int launch_cg_fit_PS(const double *y, int64_t ld, int n, int64_t N, int q, int I, const double *init,
                      const int32_t *init_status, double *coef_out, double *ll_out, int32_t *status_out,
                      int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out, unsigned long long *ctl,
                      int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready, int join_express,
-                     hipStream_t s) {
+                     int variant, unsigned char *slot_mem, hipStream_t s) {
     return with_order(q, [&](auto Qc) {
         return with_bool(I, [&](auto Ic) {
             {
                 constexpr int Q = decltype(Qc)::value, II = decltype(Ic)::value;
-                if constexpr (P + Q + II == 0) {
+                constexpr int K = P + Q + II;
+                if constexpr (K == 0) {
                     return ARIMA_E_INVALID_ARG;
+                } else if (variant == 1) {
+                    if (!slot_mem) return ARIMA_E_INVALID_ARG;
+                    if (n > express_max_n<K>(kFitGExpressLds)) express_blocks = 0;
+                    hipLaunchKernelGGL((k_cg_fit_g<P, Q, II, S, kFitGSlots>), dim3(grid_blocks + express_blocks),
+                                       dim3(64), 0, s, y, ld, n, N, init, init_status, coef_out, ll_out, status_out,
+                                       n_eval_out, n_grad_out, flags_out, ctl, xq, xready, grid_blocks, join_express,
+                                       slot_mem);
+                    STS_CHECK_LAUNCH();
+                    return ARIMA_OK;
                 } else {
-                    constexpr int SPW = fit_slots_per_wave<P + Q + II>();
+                    constexpr int SPW = fit_slots_per_wave<K>();
                     // express blocks only when the row fits next to the state in one wave's LDS share
-                    const int lds_per_wave = SPW * (int)sizeof(FitSlot<P + Q + II>);
-                    if (n > express_max_n<P + Q + II>(lds_per_wave)) express_blocks = 0;
+                    const int lds_per_wave = SPW * (int)sizeof(FitSlot<K>);
+                    if (n > express_max_n<K>(lds_per_wave)) express_blocks = 0;
                     hipLaunchKernelGGL((k_cg_fit<P, Q, II, S, SPW>), dim3(grid_blocks + express_blocks),
                                        dim3(64 * kFitWaves), 0, s, y, ld, n, N, init, init_status, coef_out, ll_out,
                                        status_out, n_eval_out, n_grad_out, flags_out, ctl, xq, xready, grid_blocks,
@@ -1070,23 +1087,23 @@ int launch_cg_fit_P(const double *y, int64_t ld, int n, int64_t N, int q, int I,
                     const int32_t *init_status, double *coef_out, double *ll_out, int32_t *status_out,
                     int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out, unsigned long long *ctl,
                     int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready, int join_express,
-                    hipStream_t s) {
+                    int variant, unsigned char *slot_mem, hipStream_t s) {
     return with_smear(smear, [&](auto Sc) {
         return launch_cg_fit_PS<P, (decltype(Sc)::value != 0)>(y, ld, n, N, q, I, init, init_status, coef_out, ll_out,
                                                                status_out, n_eval_out, n_grad_out, flags_out, ctl,
                                                                grid_blocks, express_blocks, xq, xready, join_express,
-                                                               s);
+                                                               variant, slot_mem, s);
     });
 }
 
 // series one workgroup keeps in flight (blocks of the grid are sized from it)
 template <int P>
-int cg_fit_series_per_block_P(int q, int I) {
+int cg_fit_series_per_block_P(int q, int I, int variant) {
     return with_order(q, [&](auto Qc) {
         return with_bool(I, [&](auto Ic) {
             constexpr int Q = decltype(Qc)::value, II = decltype(Ic)::value;
             if constexpr (P + Q + II == 0) return 0;
-            else return kFitWaves * fit_slots_per_wave<P + Q + II>();
+            else return variant == 1 ? kFitGSlots : kFitWaves * fit_slots_per_wave<P + Q + II>();
         });
     });
 }
@@ -1138,7 +1155,8 @@ int launch_model_flags_P(const double *coef, int64_t N, int q, int I, uint8_t *f
     EXT template int launch_cg_fit_PS<PP, SS>(const double *, int64_t, int, int64_t, int, int, const double *,    \
                                               const int32_t *, double *, double *, int32_t *, int32_t *,        \
                                               int32_t *, uint8_t *, unsigned long long *, int, int,             \
-                                              unsigned char *, unsigned *, int, hipStream_t);
+                                              unsigned char *, unsigned *, int, int, unsigned char *,           \
+                                              hipStream_t);
 
 #define STS_DECLARE_P(PP, EXT)                                                                                  \
     STS_DECLARE_CG(PP, false, extern)                                                                           \
@@ -1150,8 +1168,8 @@ int launch_model_flags_P(const double *coef, int64_t N, int q, int I, uint8_t *f
     EXT template int launch_cg_fit_P<PP>(const double *, int64_t, int, int64_t, int, int, int, const double *,   \
                                          const int32_t *, double *, double *, int32_t *, int32_t *, int32_t *,  \
                                          uint8_t *, unsigned long long *, int, int, unsigned char *, unsigned *, \
-                                         int, hipStream_t);                                                     \
-    EXT template int cg_fit_series_per_block_P<PP>(int, int);                                                   \
+                                         int, int, unsigned char *, hipStream_t);                               \
+    EXT template int cg_fit_series_per_block_P<PP>(int, int, int);                                                   \
     EXT template int launch_css_loglik_P<PP>(const double *, int64_t, int, int64_t, int, int, const double *,    \
                                              double *, hipStream_t);                                            \
     EXT template int launch_css_grad_P<PP>(const double *, int64_t, int, int64_t, int, int, int, const double *, \

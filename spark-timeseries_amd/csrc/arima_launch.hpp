@@ -26,7 +26,7 @@ int launch_cg_fit(const double *y, int64_t ld, int n, int64_t N, int p, int q, i
                   const double *init, const int32_t *init_status, double *coef_out, double *ll_out,
                   int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
                   unsigned long long *ctl, int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready,
-                  int join_express, hipStream_t s);
+                  int join_express, int variant, unsigned char *slot_mem, hipStream_t s);
 constexpr int kExpressRingEntries = 32768;      // k_cg_fit's express hand-offs per launch (entries never reused)
 constexpr int kExpressRingBytes = kExpressRingEntries * 512;   // x kExpressEntryBytes
 constexpr int kExpressReadyBytes = kExpressRingEntries * 4;
@@ -38,7 +38,11 @@ int launch_model_flags(const double *coef, int64_t N, int p, int q, int I, uint8
 // base_host: I + p + q host doubles (passed to the kernel by value)
 int launch_sample(double *out, int64_t ld, int64_t N, int T, int p, int d, int q, int I, const double *base_host,
                   double jitter, uint64_t seed, int64_t first, hipStream_t s);
-int cg_fit_series_per_block(int p, int q, int I);   // optimizer slots of one k_cg_fit workgroup
+int cg_fit_series_per_block(int p, int q, int I, int variant);   // optimizer slots of one fit workgroup
+// k_cg_fit_g (variant 1): two single-wave workgroups per SIMD, slot records of kFitGSlotBytes in global memory
+constexpr int kFitGBlocksPerCU = 8;
+constexpr int kFitGSlotsPerWave = 128;      // = kFitGSlots (arima_fit_global.hpp, checked there)
+constexpr int kFitGSlotBytes = 512;         // >= sizeof(GSlot<K>) for every K <= 11
 // k_cg_fit workgroups are single waves (4 per CU, one per SIMD, each with a quarter of the LDS): a wave that has
 // finished its series leaves the CU at once, so the next fit's waves take its SIMD and LDS share while the other
 // waves of the CU still run their slowest series (pipelined fits)

@@ -63,6 +63,7 @@ struct PendingStats {
 // Device workspace of one fit in flight: Hannan-Rissanen init, the fit kernel's counters and its express ring.
 struct FitWs {
     DevBuf init, hr_status, ctl, xring, xready;
+    DevBuf slots;            // k_cg_fit_g's optimizer slot records (fit_kernel = 1)
 };
 
 // One lane of the order search's concurrent fits (arima_order_search_batch*): its own stream, workspace and
@@ -129,6 +130,7 @@ struct arima_handle {
     int grid_blocks_override = 0;
     int express_blocks = -1;       // k_cg_fit express workgroups (-1: num_cus / 16)
     int express_ring = 0;          // express hand-offs per launch (0: the whole ring, sts::kExpressRingEntries)
+    int fit_kernel = 0;            // 0: k_cg_fit (LDS slots, 1 wave/SIMD); 1: k_cg_fit_g (global slots, 2 waves/SIMD)
     int64_t last_express = 0;
     int64_t last_grid = 0;
     int search_lanes = 8;          // concurrent fits of the order search (2/4/8: 1269/1303/1408 series/s, profiles/r02/g_c5)
@@ -376,6 +378,7 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
     if (!h || !name) return ARIMA_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
     if (!strcmp(name, "smear")) { h->smear = value ? 1 : 0; return ARIMA_OK; }
+    if (!strcmp(name, "fit_kernel")) { h->fit_kernel = value ? 1 : 0; return ARIMA_OK; }
     if (!strcmp(name, "express_ring")) {
         h->express_ring = (int)std::min<int64_t>(sts::kExpressRingEntries, std::max<int64_t>(0, value));
         return ARIMA_OK;
@@ -397,6 +400,23 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
     if (!strcmp(name, "host_chunk")) { h->host_chunk = std::max<int64_t>(1, value); return ARIMA_OK; }
     if (!strcmp(name, "fit_slice_bytes")) { h->fit_slice_bytes = std::max<int64_t>(1, value); return ARIMA_OK; }
     return set_err(h, ARIMA_E_INVALID_ARG, "unknown option");
+}
+
+int arima_get_option(const arima_handle *hc, const char *name, int64_t *value) {
+    if (!hc || !name || !value) return ARIMA_E_INVALID_ARG;
+    const arima_handle *h = hc;
+    std::lock_guard<std::mutex> lk(h->mu);
+    const struct { const char *n; int64_t v; } opts[] = {
+        {"smear", h->smear}, {"express_blocks", h->express_blocks}, {"grid_blocks", h->grid_blocks_override},
+        {"search_lanes", h->search_lanes}, {"fit_pipeline", h->pipeline}, {"host_pipeline", h->host_pipeline},
+        {"host_chunk", h->host_chunk}, {"fit_slice_bytes", h->fit_slice_bytes}, {"express_ring", h->express_ring},
+        {"fit_kernel", h->fit_kernel}};
+    for (const auto &o : opts)
+        if (!strcmp(name, o.n)) {
+            *value = o.v;
+            return ARIMA_OK;
+        }
+    return ARIMA_E_INVALID_ARG;
 }
 
 // ---------------------------------------------------------------------------------------------------------
@@ -476,9 +496,11 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
     if (xcus >= cus) xcus = cus - 1;
     int bcus = h->grid_blocks_override;
     if (bcus <= 0) bcus = std::max(1, cus - xcus);
-    int xblocks = xcus * sts::kFitBlocksPerCU;
-    int blocks = bcus * sts::kFitBlocksPerCU;
-    const int per_block = std::max(1, sts::cg_fit_series_per_block(p, q, I));
+    const int variant = h->fit_kernel;
+    const int bpc = variant == 1 ? sts::kFitGBlocksPerCU : sts::kFitBlocksPerCU;
+    int xblocks = xcus * bpc;
+    int blocks = bcus * bpc;
+    const int per_block = std::max(1, sts::cg_fit_series_per_block(p, q, I, variant));
     const int64_t need = (N + per_block - 1) / per_block;
     if (blocks > need) blocks = (int)need;
     if (xblocks > 0) {
@@ -486,11 +508,14 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
         RCCHK(h, ws.xready.ensure(sts::kExpressReadyBytes), "workspace");
         HIPCHK(h, hipMemsetAsync(ws.xready.ptr, 0, sts::kExpressReadyBytes, s));
     }
+    if (variant == 1)
+        RCCHK(h, ws.slots.ensure((size_t)blocks * sts::kFitGSlotsPerWave * sts::kFitGSlotBytes), "workspace");
     *grid_out = blocks;
     *express_out = xcus;                    // in CUs, the unit of the "express_blocks" option
     RCCHK(h, sts::launch_cg_fit(y, ldn, n, N, p, q, I, h->smear, init, init_status, d_coef, d_ll, d_status, d_neval,
                                 d_ngrad, d_flags, ws.ctl.as<unsigned long long>(), blocks, xblocks,
-                                ws.xring.as<unsigned char>(), ws.xready.as<unsigned>(), shared_gpu ? 0 : 1, s),
+                                ws.xring.as<unsigned char>(), ws.xready.as<unsigned>(), shared_gpu ? 0 : 1, variant,
+                                ws.slots.as<unsigned char>(), s),
           "cg_fit");
     hipLaunchKernelGGL(k_fault_merge, dim3(1), dim3(64), 0, s, ws.ctl.as<unsigned long long>(),
                        h->dev_fault.as<unsigned long long>());
@@ -509,6 +534,9 @@ static int reserve_fit_ws(arima_handle *h, int count, int64_t N, int64_t ldn, in
         RCCHK(h, c.ws.ctl.ensure(kCtlWords * sizeof(unsigned long long)), "workspace");
         RCCHK(h, c.ws.xring.ensure(sts::kExpressRingBytes), "workspace");
         RCCHK(h, c.ws.xready.ensure(sts::kExpressReadyBytes), "workspace");
+        if (h->fit_kernel == 1)
+            RCCHK(h, c.ws.slots.ensure((size_t)std::max(1, h->num_cus) * sts::kFitGBlocksPerCU *
+                                       sts::kFitGSlotsPerWave * sts::kFitGSlotBytes), "workspace");
     }
     return ARIMA_OK;
 }
@@ -1097,6 +1125,9 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
         if (rc == ARIMA_OK) rc = ln.ws.ctl.ensure(kCtlWords * sizeof(unsigned long long));
         if (rc == ARIMA_OK) rc = ln.ws.xring.ensure(sts::kExpressRingBytes);
         if (rc == ARIMA_OK) rc = ln.ws.xready.ensure(sts::kExpressReadyBytes);
+        if (rc == ARIMA_OK && h->fit_kernel == 1)
+            rc = ln.ws.slots.ensure((size_t)std::max(1, h->num_cus) * sts::kFitGBlocksPerCU * sts::kFitGSlotsPerWave *
+                                    sts::kFitGSlotBytes);
         if (rc != ARIMA_OK) {
             if (j == 0) return set_err(h, rc, "order search workspace");
             break;                                 // fewer lanes instead of failing the call

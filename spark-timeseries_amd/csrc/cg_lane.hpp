@@ -184,11 +184,23 @@ struct CGLane {
     STS_HD STS_FI void spec_store(int h, double f) {
         if constexpr (NC > 0) {
             const int slot = sp_next;
-            sp_alpha[slot] = rq_spec[h];
-            sp_f[slot] = f;
+            const double al = rq_spec[h];
+#pragma unroll
+            for (int s = 0; s < NC; ++s)            // static indices: the state can live in registers
+                if (s == slot) {
+                    sp_alpha[s] = al;
+                    sp_f[s] = f;
+                }
             sp_next = (uint8_t)(slot + 1 == NC ? 0 : slot + 1);
             if (sp_n < NC) sp_n++;
         }
+    }
+
+    // start() plus what advance() does at PC_START: post G at the initial point (a refill needs no advance call)
+    STS_HD STS_FI void start_posted(const double (&init)[K]) {
+        start(init);
+        req = REQ_G;
+        pc = PC_G0;
     }
 
   private:
@@ -288,7 +300,11 @@ struct CGLane {
   public:
     // Run the state machine until a request is posted (req != REQ_NONE) or the fit is finished. fr / gr are
     // the response to the request served last (objective; and the gradient for a G request).
-    STS_HD void advance(double fr, const double (&gr)[K]) {
+    // out-of-line: the LDS-resident slots of the bulk kernel and the express path call it through a pointer
+    STS_HD void advance(double fr, const double (&gr)[K]) { step(fr, gr); }
+
+    // the state machine itself, force-inlined where the lane's state is a register-resident copy
+    STS_HD STS_FI void step(double fr, const double (&gr)[K]) {
         const double GS = brent_gs();
         double ev_val = fr;                                   // objective value delivered to the resume point
         double grad[K];                                       // gradient delivered to PC_G0 / PC_G

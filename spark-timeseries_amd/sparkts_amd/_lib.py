@@ -44,7 +44,7 @@ DEFAULT_SMEAR = 1
 # every symbol include/sparkts_arima.h declares (checked by tests/test_abi.py)
 EXPORTED = [
     "arima_create", "arima_destroy", "arima_last_error", "arima_status_name", "arima_num_params",
-    "arima_get_last_stats", "arima_set_option", "arima_fit_batch", "arima_fit_batch_device",
+    "arima_get_last_stats", "arima_set_option", "arima_get_option", "arima_fit_batch", "arima_fit_batch_device",
     "arima_difference_batch", "arima_inverse_difference_batch", "arima_css_loglik_batch",
     "arima_css_gradient_batch", "arima_hannan_rissanen_batch", "arima_forecast_batch", "arima_model_flags_batch",
     "arima_sample_batch_device", "arima_order_search_batch", "arima_order_search_batch_device",
@@ -116,6 +116,7 @@ def load():
         L.arima_num_params.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.arima_get_last_stats.argtypes = [H, ctypes.POINTER(FitStats)]
         L.arima_set_option.argtypes = [H, ctypes.c_char_p, _i64]
+        L.arima_get_option.argtypes = [H, ctypes.c_char_p, ctypes.POINTER(_i64)]
         L.arima_synchronize.argtypes = [H]
         L.arima_fit_batch.argtypes = [H, _dp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _dp, _dp, _dp, _i32p,
                                       _i32p, _i32p, _u8p]
@@ -156,6 +157,9 @@ class Engine:
             raise EngineError(f"arima_create(device={device}) failed with {rc}: no usable HIP device")
         self.h = h
         self.device = device
+        # engine-wide knobs from the environment (A/B runs of the test suite and the bench): SPARKTS_FIT_KERNEL=0|1
+        if os.environ.get("SPARKTS_FIT_KERNEL", "") != "":
+            self.set_option("fit_kernel", int(os.environ["SPARKTS_FIT_KERNEL"]))
 
     @classmethod
     def get(cls, device=None):
@@ -176,6 +180,11 @@ class Engine:
 
     def set_option(self, name, value):
         self._check(self.L.arima_set_option(self.h, name.encode(), int(value)), "arima_set_option")
+
+    def get_option(self, name):
+        v = _i64()
+        self._check(self.L.arima_get_option(self.h, name.encode(), ctypes.byref(v)), "arima_get_option")
+        return int(v.value)
 
     def synchronize(self):
         """Wait for the device work of every call issued on this handle (the *_device calls are asynchronous)."""
