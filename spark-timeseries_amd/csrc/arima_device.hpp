@@ -421,6 +421,11 @@ __device__ __forceinline__ void grad_column_lds(const double *row, int n,
 // first_elem(r) (series index of the element that completes row r), push(v, x, y) (next row from the next
 // series element).
 // ------------------------------------------------------------------------------------------------------
+#ifndef STS_HR_PF
+#define STS_HR_PF 2
+#endif
+constexpr int kPrefetchHR = STS_HR_PF;   // 128-B chunks in flight per lane in the Householder passes
+
 template <int C>
 struct HouseholderState {
     double a[C];          // rDiag
@@ -462,7 +467,7 @@ __device__ __forceinline__ int ols_stage(Gen &gen, const double *__restrict__ ro
             xnorm = (double)R;
         } else if (S + 1 < R) {
             gen.begin(S + 1);
-            stream_elems<2>(row, gen.first_elem(S + 1), n, [&](double v) {
+            stream_elems<kPrefetchHR>(row, gen.first_elem(S + 1), n, [&](double v) {
                 double x[C], y;
                 gen.push(v, x, y);
                 hh_apply<C>(H, S, x, y);
@@ -481,7 +486,7 @@ __device__ __forceinline__ int ols_stage(Gen &gen, const double *__restrict__ ro
         dt = 0.0 + ys * vt;
         if (S + 1 < R) {
             gen.begin(S + 1);
-            stream_elems<2>(row, gen.first_elem(S + 1), n, [&](double v) {
+            stream_elems<kPrefetchHR>(row, gen.first_elem(S + 1), n, [&](double v) {
                 double x[C], y;
                 gen.push(v, x, y);
                 hh_apply<C>(H, S, x, y);

@@ -546,9 +546,9 @@ STS_DECLARE_P(5, extern)
 #endif
 
 int launch_hr_init(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, double *init_out,
-                   int32_t *status_out, hipStream_t s) {
+                   int32_t *status_out, hipStream_t s, int hr_grid) {
     if (N == 0) return ARIMA_OK;
-#define C_(PP) launch_hr_init_P<PP>(y, ld, n, N, q, I, init_out, status_out, s)
+#define C_(PP) launch_hr_init_P<PP>(y, ld, n, N, q, I, init_out, status_out, s, hr_grid)
     STS_P_SWITCH(C_)
 #undef C_
 }

@@ -1007,16 +1007,15 @@ inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 
 
 template <int P>
 int launch_hr_init_P(const double *y, int64_t ld, int n, int64_t N, int q, int I, double *init_out,
-                     int32_t *status_out, hipStream_t s) {
+                     int32_t *status_out, hipStream_t s, int hr_grid) {
     return with_order(q, [&](auto Qc) {
         return with_bool(I, [&](auto Ic) {
             constexpr int Q = decltype(Qc)::value, II = decltype(Ic)::value;
-#ifdef STS_HR_BLOCKS
-            const unsigned grid = std::min<unsigned>(grid_for(N, 256), STS_HR_BLOCKS);
-#else
-            const unsigned grid = grid_for(N, 256);
-#endif
-            hipLaunchKernelGGL((k_hr_init<P, Q, II>), dim3(grid), dim3(256), 0, s, y, ld, n, N, init_out, status_out);
+            const int block = hr_grid > 0 ? 64 : 256;
+            const unsigned grid =
+                hr_grid > 0 ? std::min<unsigned>(grid_for(N, 64), (unsigned)hr_grid) : grid_for(N, 256);
+            hipLaunchKernelGGL((k_hr_init<P, Q, II>), dim3(grid), dim3(block), 0, s, y, ld, n, N, init_out,
+                               status_out);
             STS_CHECK_LAUNCH();
             return ARIMA_OK;
         });
@@ -1162,7 +1161,7 @@ int launch_model_flags_P(const double *coef, int64_t N, int q, int I, uint8_t *f
     STS_DECLARE_CG(PP, false, extern)                                                                           \
     STS_DECLARE_CG(PP, true, extern)                                                                            \
     EXT template int launch_hr_init_P<PP>(const double *, int64_t, int, int64_t, int, int, double *, int32_t *,  \
-                                          hipStream_t);                                                         \
+                                          hipStream_t, int);                                                    \
     EXT template int launch_ar_fit_P<PP>(const double *, int64_t, int, int64_t, int, double *, double *,         \
                                          int32_t *, int32_t *, int32_t *, uint8_t *, hipStream_t);              \
     EXT template int launch_cg_fit_P<PP>(const double *, int64_t, int, int64_t, int, int, int, const double *,   \

@@ -17,8 +17,10 @@ int launch_forecast(const double *ts, int64_t ld_in, const double *coef, int k, 
                     int64_t N, int T, int p, int d, int q, int I, int n_future, hipStream_t s);
 int launch_inverse_difference(const double *in, int64_t ld_in, double *out, int64_t ld_out, int64_t N, int T,
                               int d, hipStream_t s);
+// hr_grid > 0: that many single-wave workgroups stride over the series (bounds the rows in flight, so the 2(C_A + C_B)
+// passes over a row can hit the Infinity Cache); 0: one lane per series in 256-lane workgroups
 int launch_hr_init(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, double *init_out,
-                   int32_t *status_out, hipStream_t s);
+                   int32_t *status_out, hipStream_t s, int hr_grid = 0);
 int launch_ar_fit(const double *y, int64_t ld, int n, int64_t N, int p, int I, double *coef_out, double *ll_out,
                   int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
                   hipStream_t s);

@@ -130,6 +130,7 @@ struct arima_handle {
     int grid_blocks_override = 0;
     int express_blocks = -1;       // k_cg_fit express workgroups (-1: num_cus / 16)
     int express_ring = 0;          // express hand-offs per launch (0: the whole ring, sts::kExpressRingEntries)
+    int hr_grid = 0;               // k_hr_init: 0 = a lane per series; > 0 = that many single-wave workgroups
     int fit_kernel = 0;            // 0: k_cg_fit (LDS slots, 1 wave/SIMD); 1: k_cg_fit_g (global slots, 2 waves/SIMD)
     int64_t last_express = 0;
     int64_t last_grid = 0;
@@ -379,6 +380,7 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
     std::lock_guard<std::mutex> lk(h->mu);
     if (!strcmp(name, "smear")) { h->smear = value ? 1 : 0; return ARIMA_OK; }
     if (!strcmp(name, "fit_kernel")) { h->fit_kernel = value ? 1 : 0; return ARIMA_OK; }
+    if (!strcmp(name, "hr_grid")) { h->hr_grid = (int)std::min<int64_t>(1 << 20, std::max<int64_t>(0, value)); return ARIMA_OK; }
     if (!strcmp(name, "express_ring")) {
         h->express_ring = (int)std::min<int64_t>(sts::kExpressRingEntries, std::max<int64_t>(0, value));
         return ARIMA_OK;
@@ -410,7 +412,7 @@ int arima_get_option(const arima_handle *hc, const char *name, int64_t *value) {
         {"smear", h->smear}, {"express_blocks", h->express_blocks}, {"grid_blocks", h->grid_blocks_override},
         {"search_lanes", h->search_lanes}, {"fit_pipeline", h->pipeline}, {"host_pipeline", h->host_pipeline},
         {"host_chunk", h->host_chunk}, {"fit_slice_bytes", h->fit_slice_bytes}, {"express_ring", h->express_ring},
-        {"fit_kernel", h->fit_kernel}};
+        {"fit_kernel", h->fit_kernel}, {"hr_grid", h->hr_grid}};
     for (const auto &o : opts)
         if (!strcmp(name, o.n)) {
             *value = o.v;
@@ -474,7 +476,8 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
     if (!d_user_init) {
         RCCHK(h, ws.init.ensure((size_t)N * std::max(k, 1) * sizeof(double)), "workspace");
         RCCHK(h, ws.hr_status.ensure((size_t)N * sizeof(int32_t)), "workspace");
-        RCCHK(h, sts::launch_hr_init(y, ldn, n, N, p, q, I, ws.init.as<double>(), ws.hr_status.as<int32_t>(), s),
+        RCCHK(h, sts::launch_hr_init(y, ldn, n, N, p, q, I, ws.init.as<double>(), ws.hr_status.as<int32_t>(), s,
+                                     h->hr_grid),
               "hr_init");
         init = ws.init.as<double>();
         init_status = ws.hr_status.as<int32_t>();
@@ -1006,7 +1009,7 @@ int arima_hannan_rissanen_batch(arima_handle *h, const double *diffed, int64_t N
     RCCHK(h, h->h_coef.ensure((size_t)N * std::max(k, 1) * sizeof(double)), "staging");
     RCCHK(h, h->h_status.ensure((size_t)N * sizeof(int32_t)), "staging");
     RCCHK(h, sts::launch_hr_init(h->diff.as<double>(), ld, n, N, p, q, I, h->h_coef.as<double>(),
-                                 h->h_status.as<int32_t>(), s), "hr_init");
+                                 h->h_status.as<int32_t>(), s, h->hr_grid), "hr_init");
     if (k > 0) HIPCHK(h, hipMemcpyAsync(init_out, h->h_coef.ptr, (size_t)N * k * sizeof(double), hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipMemcpyAsync(status_out, h->h_status.ptr, (size_t)N * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     HIPCHK(h, end_call(h, s));

@@ -160,6 +160,10 @@ class Engine:
         # engine-wide knobs from the environment (A/B runs of the test suite and the bench): SPARKTS_FIT_KERNEL=0|1
         if os.environ.get("SPARKTS_FIT_KERNEL", "") != "":
             self.set_option("fit_kernel", int(os.environ["SPARKTS_FIT_KERNEL"]))
+        # any option: SPARKTS_OPTIONS="hr_grid=1024,fit_pipeline=2"
+        for kv in filter(None, os.environ.get("SPARKTS_OPTIONS", "").split(",")):
+            name, _, val = kv.partition("=")
+            self.set_option(name.strip(), int(val))
 
     @classmethod
     def get(cls, device=None):
