@@ -198,7 +198,7 @@ def main():
     ap.add_argument("--pipeline", type=int, default=3)
     ap.add_argument("--express-blocks", type=int, default=-1, help="express workgroups of the fit kernel (-1: CUs/16)")
     ap.add_argument("--e2e", type=int, default=1, choices=[0, 1])
-    ap.add_argument("--fit-kernel", type=int, default=-1, help="0: k_cg_fit (LDS slots), 1: k_cg_fit_g; -1: default")
+    ap.add_argument("--fit-kernel", type=int, default=-1, help="0: k_cg_fit (LDS slots), 2: rounds of streaming passes; -1: default")
     ap.add_argument("--device", type=int, default=None, help="GPU of every rank (default: LOCAL_RANK's)")
     ap.add_argument("--dry-run", action="store_true")
     args = ap.parse_args()
@@ -308,6 +308,8 @@ def main():
     barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0, dist if world > 1 else None)
     s0 = eng.stats()                      # the last timed step
+    if s0["series_done"] != N:            # every series of the step must have a written result
+        raise SystemExit(f"bench.py: the last step wrote {s0['series_done']} of {N} results (fault {s0['fault']})")
     log(f"[rank {rank}] {args.steps} steps in {elapsed:.3f} s; last step: difference {s0['ms_difference']:.1f} ms, "
         f"hr {s0['ms_hr_init']:.1f} ms, cg {s0['ms_cg_fit']:.1f} ms")
 
@@ -333,6 +335,8 @@ def main():
     step()
     eng.synchronize()
     s1 = eng.stats()
+    if s1["series_done"] != N:
+        raise SystemExit(f"bench.py: the isolated step wrote {s1['series_done']} of {N} results")
     eng.set_option("fit_pipeline", args.pipeline)
     flops_iso, _, _ = cg_flops(s1)
     cg_ms = s1["ms_cg_fit"]
@@ -367,9 +371,9 @@ def main():
                        "series_per_gpu": N, "series_total": total_series, "series_len": T,
                        "parallelism": f"series-sharded x{world}, no collective",
                        "breeze_overlap": "smear" if args.smear else "shift",
-                       "fit_kernel": "k_cg_fit_g (slot records in HBM, 2 waves/SIMD)" if eng_fit_kernel(eng) == 1
-                       else "k_cg_fit (LDS slots, 1 wave/SIMD)",
-                       "converged_fraction": conv,
+                       "fit_kernel": "rounds (k_rounds_pass / k_rounds_advance, then k_cg_fit on the tail)"
+                       if eng_fit_kernel(eng) == 2 else "k_cg_fit (LDS slots, 1 wave/SIMD)",
+                       "converged_fraction": conv, "series_done": s0["series_done"],
                        "mean_n_eval": s0["n_eval"] / max(N, 1), "mean_n_grad": s0["n_grad"] / max(N, 1),
                        "lane_f_passes_per_series": s0["f_passes"] / max(N, 1),
                        "lane_g_passes_per_series": s0["g_passes"] / max(N, 1),

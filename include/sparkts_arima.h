@@ -97,6 +97,7 @@ typedef struct arima_fit_stats {
     int64_t fault_info[5];   /* the kernel's record of the first fault (ticket, fills, bulk waves done, ...)      */
     int64_t diag[6];         /* diagnostics of builds with -DSTS_TIMING; else 0                       */
     int64_t ride_passes;     /* objective requests served by gradient passes (counted in g_passes)    */
+    int64_t series_done;     /* series whose result the fit kernels wrote (== n_series unless a fault dropped some) */
 } arima_fit_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------------------- */
@@ -114,11 +115,16 @@ int         arima_synchronize(arima_handle *h);
  * "fit_pipeline" (fit contexts in rotation for *_device fits, 1..4, default 1), "host_chunk" / "host_pipeline"
  * (series per chunk and contexts of the chunked host path, default 262144 / 3), "express_blocks",
  * "grid_blocks", "search_lanes" (in-kernel scheduler and order-search concurrency), "fit_kernel" (0: k_cg_fit with
- * LDS-resident optimizer slots, 1: k_cg_fit_g with slot records in HBM and two waves per SIMD), "fit_slice_bytes"
+ * LDS-resident optimizer slots; 2: rounds of streaming passes, then k_cg_fit on the last series), "rounds_max",
+ * "rounds_tail", "rounds_pass_waves" (fit_kernel 2), "hr_grid" (k_hr_init grid), "fit_slice_bytes"
  * (differenced workspace of one slice of a large device fit), "express_ring" (express hand-offs per launch). */
 int         arima_set_option(arima_handle *h, const char *name, int64_t value);
 /* Current value of a tuning knob (the names arima_set_option takes); ARIMA_E_INVALID_ARG for an unknown name. */
 int         arima_get_option(const arima_handle *h, const char *name, int64_t *value);
+/* Diagnostics (fit_kernel 2): waits for the last device fit and copies its round-control words (per round: the
+ * request counts of lists G, F+2, F+1, F+0 and the pass kernel's tile counter, 8 words a round; the tail count
+ * after the last round) into out[0 .. max_words). Returns the number of words written, or a negative error. */
+int         arima_rounds_trace(arima_handle *h, unsigned *out, int max_words);
 
 /* ---- ARIMA.fitModel over a batch (ARIMA.scala:79-116) ----------------------------------------------- *
  * series    N x T host, series-major                 user_init  NULL (Hannan-Rissanen, ARIMA.scala:216) or N x k

@@ -566,12 +566,12 @@ int launch_cg_fit(const double *y, int64_t ld, int n, int64_t N, int p, int q, i
                   const double *init, const int32_t *init_status, double *coef_out, double *ll_out,
                   int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
                   unsigned long long *ctl, int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready,
-                  int join_express, int variant, unsigned char *slot_mem, hipStream_t s) {
+                  int join_express, int variant, const FitRounds *rounds, hipStream_t s) {
     if (N == 0) return ARIMA_OK;
 #define C_(PP)                                                                                             \
     launch_cg_fit_P<PP>(y, ld, n, N, q, I, smear, init, init_status, coef_out, ll_out, status_out, n_eval_out, \
                         n_grad_out, flags_out, ctl, grid_blocks, express_blocks, xq, xready, join_express, variant, \
-                        slot_mem, s)
+                        rounds, s)
     STS_P_SWITCH(C_)
 #undef C_
 }
@@ -608,4 +608,20 @@ int launch_model_flags(const double *coef, int64_t N, int p, int q, int I, uint8
 int hr_shape_status_host(int n, int p, int q, int I) { return hr_shape_status(n, p, q, I); }
 int ar_shape_status_host(int n, int p, int I) { return ar_shape_status(n, p, I); }
 
+}  // namespace sts
+
+namespace sts {
+int rounds_rec_bytes(int k) {
+    switch (k) {
+#define RC_(KK) case KK: return rounds_rec_stride<KK>();
+        RC_(1) RC_(2) RC_(3) RC_(4) RC_(5) RC_(6) RC_(7) RC_(8) RC_(9) RC_(10) RC_(11)
+#undef RC_
+    default: return 0;
+    }
+}
+int rounds_resp_words(int k) { return k >= 1 && k <= 11 ? 1 + spec_ns<5>() + k : 0; }
+}  // namespace sts
+
+namespace sts {
+int64_t rounds_ranges(int64_t N) { return (N + kRangeSeries - 1) / kRangeSeries; }
 }  // namespace sts

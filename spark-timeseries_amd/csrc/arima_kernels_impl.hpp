@@ -379,7 +379,7 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
     FitSlotCore<K> &ES = *reinterpret_cast<FitSlotCore<K> *>(gbase);
     double *row = reinterpret_cast<double *>(gbase + express_state_bytes<K>());
     double *xch = row + ((n + 1) & ~1);                     // K + NS + 1 doubles
-    unsigned long long served = 0, pf = 0, pg = 0, evals = 0, grads = 0, hits = 0;
+    unsigned long long served = 0, pf = 0, pg = 0, evals = 0, grads = 0, hits = 0, done = 0;
     // group state: 0 = waiting on ticket, 1 = fitting, 2 = retired (wave-uniform per group after each shfl)
     int gstate = 0;
     unsigned long long ticket = 0;
@@ -518,6 +518,7 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
             evals += ES.s.n_eval;
             grads += ES.s.n_grad;
             hits += ES.s.spec_hits;
+            done++;
             ticket = add_agent(&ctl[20], 1ull);
             tk_time = __builtin_amdgcn_s_memrealtime();
             tk_polls = 0;
@@ -531,6 +532,7 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
         atomicAdd(&ctl[5], evals);
         atomicAdd(&ctl[6], grads);
         atomicAdd(&ctl[7], hits);
+        atomicAdd(&ctl[32], done);
         atomicAdd(&ctl[23], served);
         atomicAdd(&ctl[24], pf);
         atomicAdd(&ctl[25], pg);
@@ -543,7 +545,10 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
     const int32_t *__restrict__ init_status, double *__restrict__ coef_out, double *__restrict__ ll_out,
     int32_t *__restrict__ status_out, int32_t *__restrict__ n_eval_out, int32_t *__restrict__ n_grad_out,
     uint8_t *__restrict__ flags_out, unsigned long long *__restrict__ ctl, unsigned char *__restrict__ xq,
-    unsigned *__restrict__ xready, int n_bulk, int join_express) {
+    unsigned *__restrict__ xready, int n_bulk, int join_express, const int32_t *__restrict__ resume_list,
+    const unsigned *__restrict__ resume_n, const unsigned char *__restrict__ resume_rec) {
+    // resume_list != nullptr: the launch fits the *resume_n series listed there from their optimizer states in
+    // resume_rec (the records of arima_fit_rounds.hpp; init / init_status unused) instead of series 0..N-1.
     // ctl[0] = work counter, ctl[1] = lane F passes, ctl[2] = lane G passes, ctl[3] = wave F passes (one chain),
     // ctl[4] = wave G passes, ctl[5] = objective evaluations, ctl[6] = gradient evaluations, ctl[7] = spec hits,
     // ctl[8] = wave F passes with speculative chains, ctl[9] = speculative chains evaluated,
@@ -559,6 +564,7 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
     __shared__ int assign[kFitWaves][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const bool has_express = n_bulk < (int)gridDim.x;
+    if (resume_list) N = (int64_t)*resume_n;             // written by the previous kernel (stream order)
     if ((int)blockIdx.x >= n_bulk) {                      // express workgroup: this wave's share of the LDS
         fit_express<P, Q, I, SMEAR>(reinterpret_cast<unsigned char *>(&slots[wave][0]), (int)sizeof(slots[0]), y, ld,
                                     n, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out, ctl, xq,
@@ -573,7 +579,7 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
     FitSlot<K> *ws = slots[wave];
     const unsigned long long xring = express_ring_entries(ctl);
     unsigned long long lane_f = 0, lane_g = 0, wave_f = 0, wave_g = 0, wave_m = 0, evals = 0, grads = 0, hits = 0,
-                       chains = 0, rides = 0;
+                       chains = 0, rides = 0, done = 0;
     unsigned round_no = 0;
     bool drained = false;                  // the batch's work counter has run out (this wave saw it)
     const bool lane0 = lane == 0;
@@ -608,6 +614,16 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
                     S.sid = -1;
                     S.s.req = REQ_NONE;
                     need = false;
+                } else if (resume_list) {             // a series of the rounds, with its request posted
+                    const int64_t rs = resume_list[sid];
+                    S.s = *reinterpret_cast<const CGLane<K, NS, spec_nc<K>()> *>(
+                        resume_rec + rs * (int64_t)((sizeof(CGLane<K, NS, spec_nc<K>()>) + 127) / 128 * 128));
+                    S.sid = rs;
+#ifdef STS_TIMING
+                    S.t_start = (double)__builtin_amdgcn_s_memrealtime();
+                    S.t_donate = 0.0;
+#endif
+                    need = false;
                 } else {
                     const int st0 = init_status ? init_status[sid] : ARIMA_ST_OK;
                     if (st0 != ARIMA_ST_OK) {
@@ -616,6 +632,7 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
                         for (int j = 0; j < K; ++j) nanc[j] = __builtin_nan("");
                         write_fit<K>(sid, st0, nanc, 0.0, 0, 0, 0, coef_out, ll_out, status_out, n_eval_out,
                                      n_grad_out, flags_out);
+                        done++;
                     } else {
                         double x0[K], g0[K];
 #pragma unroll
@@ -787,6 +804,7 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
                 evals += S.s.n_eval;
                 grads += S.s.n_grad;
                 hits += S.s.spec_hits;
+                done++;
                 need = true;
             }
         }
@@ -905,11 +923,12 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
     atomicAdd(&ctl[7], hits);
     atomicAdd(&ctl[9], chains);
     atomicAdd(&ctl[18], rides);
+    atomicAdd(&ctl[32], done);
 }
 
 }  // namespace sts
 
-#include "arima_fit_global.hpp"
+#include "arima_fit_rounds.hpp"
 
 namespace sts {
 
@@ -1041,13 +1060,14 @@ int launch_ar_fit_P(const double *y, int64_t ld, int n, int64_t N, int I, double
 
 // k_cg_fit launcher for one AR order and Breeze reading (each instantiated in its own translation unit,
 // arima_cg_p<P>_s<S>.hip, so the build parallelises over the heaviest kernel). variant 0: k_cg_fit (LDS slots, one
-// wave per SIMD); variant 1: k_cg_fit_g (slot records in slot_mem, two waves per SIMD).
+// wave per SIMD); variant 2: rounds of streaming passes (arima_fit_rounds.hpp) until few series are left, then
+// k_cg_fit resumes those from their records.
 template <int P, bool S>
 int launch_cg_fit_PS(const double *y, int64_t ld, int n, int64_t N, int q, int I, const double *init,
                      const int32_t *init_status, double *coef_out, double *ll_out, int32_t *status_out,
                      int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out, unsigned long long *ctl,
                      int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready, int join_express,
-                     int variant, unsigned char *slot_mem, hipStream_t s) {
+                     int variant, const FitRounds *rounds, hipStream_t s) {
     return with_order(q, [&](auto Qc) {
         return with_bool(I, [&](auto Ic) {
             {
@@ -1055,24 +1075,50 @@ int launch_cg_fit_PS(const double *y, int64_t ld, int n, int64_t N, int q, int I
                 constexpr int K = P + Q + II;
                 if constexpr (K == 0) {
                     return ARIMA_E_INVALID_ARG;
-                } else if (variant == 1) {
-                    if (!slot_mem) return ARIMA_E_INVALID_ARG;
-                    if (n > express_max_n<K>(kFitGExpressLds)) express_blocks = 0;
-                    hipLaunchKernelGGL((k_cg_fit_g<P, Q, II, S, kFitGSlots>), dim3(grid_blocks + express_blocks),
-                                       dim3(64), 0, s, y, ld, n, N, init, init_status, coef_out, ll_out, status_out,
-                                       n_eval_out, n_grad_out, flags_out, ctl, xq, xready, grid_blocks, join_express,
-                                       slot_mem);
-                    STS_CHECK_LAUNCH();
-                    return ARIMA_OK;
                 } else {
                     constexpr int SPW = fit_slots_per_wave<K>();
                     // express blocks only when the row fits next to the state in one wave's LDS share
                     const int lds_per_wave = SPW * (int)sizeof(FitSlot<K>);
                     if (n > express_max_n<K>(lds_per_wave)) express_blocks = 0;
+                    const int32_t *resume_list = nullptr;
+                    const unsigned *resume_n = nullptr;
+                    const unsigned char *resume_rec = nullptr;
+                    if (variant == 2) {                   // rounds of streaming passes, then k_cg_fit on the rest
+                        if (!rounds || rounds->max_rounds < 1) return ARIMA_E_INVALID_ARG;
+                        const FitRounds &R = *rounds;
+                        unsigned *tail_n = R.rc + (size_t)(R.max_rounds + 1) * kRcStride;
+                        const int nranges = (int)((N + kRangeSeries - 1) / kRangeSeries);
+                        auto compact = [&](int ro) {       // marks -> round ro's lists (+ the tail list)
+                            hipLaunchKernelGGL(k_rounds_count, dim3(nranges), dim3(64), 0, s, N, R.mark, R.counts);
+                            hipLaunchKernelGGL(k_rounds_scan, dim3(1), dim3(1024), 0, s, nranges, R.counts,
+                                               R.rc + (size_t)ro * kRcStride, tail_n);
+                            hipLaunchKernelGGL(k_rounds_scatter, dim3(nranges), dim3(64), 0, s, N, R.mark, R.counts,
+                                               R.lists + (size_t)(ro & 1) * kRoundLists * N, R.tail);
+                        };
+                        hipLaunchKernelGGL((k_rounds_init<K>), dim3(grid_for(N, 64)), dim3(64), 0, s, N, init,
+                                           init_status, R.rec, R.mark, coef_out, ll_out, status_out, n_eval_out,
+                                           n_grad_out, flags_out, ctl);
+                        compact(0);
+                        STS_CHECK_LAUNCH();
+                        for (int r = 0; r < R.max_rounds; ++r) {
+                            hipLaunchKernelGGL((k_rounds_pass<P, Q, II, S>), dim3(R.pass_blocks), dim3(64), 0, s, r, y,
+                                               ld, n, N, R.rec, R.resp, R.lists, R.rc, ctl);
+                            STS_CHECK_LAUNCH();
+                            hipLaunchKernelGGL((k_rounds_advance<P, Q, II>), dim3(R.advance_blocks), dim3(64), 0, s, r,
+                                               r == R.max_rounds - 1 ? 1 : 0, R.tail_at, N, R.rec, R.resp, R.lists,
+                                               R.rc, R.mark, coef_out, ll_out, status_out, n_eval_out, n_grad_out,
+                                               flags_out, ctl);
+                            compact(r + 1);
+                            STS_CHECK_LAUNCH();
+                        }
+                        resume_list = R.tail;
+                        resume_n = tail_n;
+                        resume_rec = R.rec;
+                    }
                     hipLaunchKernelGGL((k_cg_fit<P, Q, II, S, SPW>), dim3(grid_blocks + express_blocks),
                                        dim3(64 * kFitWaves), 0, s, y, ld, n, N, init, init_status, coef_out, ll_out,
                                        status_out, n_eval_out, n_grad_out, flags_out, ctl, xq, xready, grid_blocks,
-                                       join_express);
+                                       join_express, resume_list, resume_n, resume_rec);
                     STS_CHECK_LAUNCH();
                     return ARIMA_OK;
                 }
@@ -1086,12 +1132,12 @@ int launch_cg_fit_P(const double *y, int64_t ld, int n, int64_t N, int q, int I,
                     const int32_t *init_status, double *coef_out, double *ll_out, int32_t *status_out,
                     int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out, unsigned long long *ctl,
                     int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready, int join_express,
-                    int variant, unsigned char *slot_mem, hipStream_t s) {
+                    int variant, const FitRounds *rounds, hipStream_t s) {
     return with_smear(smear, [&](auto Sc) {
         return launch_cg_fit_PS<P, (decltype(Sc)::value != 0)>(y, ld, n, N, q, I, init, init_status, coef_out, ll_out,
                                                                status_out, n_eval_out, n_grad_out, flags_out, ctl,
                                                                grid_blocks, express_blocks, xq, xready, join_express,
-                                                               variant, slot_mem, s);
+                                                               variant, rounds, s);
     });
 }
 
@@ -1102,7 +1148,7 @@ int cg_fit_series_per_block_P(int q, int I, int variant) {
         return with_bool(I, [&](auto Ic) {
             constexpr int Q = decltype(Qc)::value, II = decltype(Ic)::value;
             if constexpr (P + Q + II == 0) return 0;
-            else return variant == 1 ? kFitGSlots : kFitWaves * fit_slots_per_wave<P + Q + II>();
+            else return kFitWaves * fit_slots_per_wave<P + Q + II>();
         });
     });
 }
@@ -1154,7 +1200,7 @@ int launch_model_flags_P(const double *coef, int64_t N, int q, int I, uint8_t *f
     EXT template int launch_cg_fit_PS<PP, SS>(const double *, int64_t, int, int64_t, int, int, const double *,    \
                                               const int32_t *, double *, double *, int32_t *, int32_t *,        \
                                               int32_t *, uint8_t *, unsigned long long *, int, int,             \
-                                              unsigned char *, unsigned *, int, int, unsigned char *,           \
+                                              unsigned char *, unsigned *, int, int, const FitRounds *,         \
                                               hipStream_t);
 
 #define STS_DECLARE_P(PP, EXT)                                                                                  \
@@ -1167,7 +1213,7 @@ int launch_model_flags_P(const double *coef, int64_t N, int q, int I, uint8_t *f
     EXT template int launch_cg_fit_P<PP>(const double *, int64_t, int, int64_t, int, int, int, const double *,   \
                                          const int32_t *, double *, double *, int32_t *, int32_t *, int32_t *,  \
                                          uint8_t *, unsigned long long *, int, int, unsigned char *, unsigned *, \
-                                         int, int, unsigned char *, hipStream_t);                               \
+                                         int, int, const FitRounds *, hipStream_t);                             \
     EXT template int cg_fit_series_per_block_P<PP>(int, int, int);                                                   \
     EXT template int launch_css_loglik_P<PP>(const double *, int64_t, int, int64_t, int, int, const double *,    \
                                              double *, hipStream_t);                                            \

@@ -24,11 +24,29 @@ int launch_hr_init(const double *y, int64_t ld, int n, int64_t N, int p, int q, 
 int launch_ar_fit(const double *y, int64_t ld, int n, int64_t N, int p, int I, double *coef_out, double *ll_out,
                   int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
                   hipStream_t s);
+// Workspaces of the rounds fit (variant 2, arima_fit_rounds.hpp), one set per fit in flight.
+constexpr int kRoundLists = 4;     // request lists per round: G, F with 2, 1, 0 predicted points
+constexpr int kRcStride = 8;       // round-control words per round (list counts, the pass kernel's tile counter)
+struct FitRounds {
+    unsigned char *rec;            // N x rounds_rec_bytes(k): the optimizer state of every series
+    double *resp;                  // N x rounds_resp_words(k): the response of its last pass
+    int32_t *lists;                // 2 x kRoundLists x N series ids (round parity)
+    int32_t *tail;                 // N: the series handed to k_cg_fit
+    uint8_t *mark;                 // N: the list of each series' next request (arima_fit_rounds.hpp)
+    unsigned *counts;              // rounds_ranges(N) x 8: per range of series, list counts, then offsets
+    unsigned *rc;                  // (max_rounds + 2) x kRcStride, zeroed before the fit; the tail count last
+    int max_rounds;                // rounds enqueued (the last one hands every unfinished series to k_cg_fit)
+    unsigned tail_at;              // a round with at most this many requests hands them to k_cg_fit
+    int pass_blocks, advance_blocks;   // persistent grids (single-wave workgroups)
+};
+int rounds_rec_bytes(int k);       // record stride of k parameters (a multiple of 128 B)
+int rounds_resp_words(int k);
+int64_t rounds_ranges(int64_t N);  // ranges of series the list compaction works on
 int launch_cg_fit(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, int smear,
                   const double *init, const int32_t *init_status, double *coef_out, double *ll_out,
                   int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
                   unsigned long long *ctl, int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready,
-                  int join_express, int variant, unsigned char *slot_mem, hipStream_t s);
+                  int join_express, int variant, const FitRounds *rounds, hipStream_t s);
 constexpr int kExpressRingEntries = 32768;      // k_cg_fit's express hand-offs per launch (entries never reused)
 constexpr int kExpressRingBytes = kExpressRingEntries * 512;   // x kExpressEntryBytes
 constexpr int kExpressReadyBytes = kExpressRingEntries * 4;
@@ -41,10 +59,6 @@ int launch_model_flags(const double *coef, int64_t N, int p, int q, int I, uint8
 int launch_sample(double *out, int64_t ld, int64_t N, int T, int p, int d, int q, int I, const double *base_host,
                   double jitter, uint64_t seed, int64_t first, hipStream_t s);
 int cg_fit_series_per_block(int p, int q, int I, int variant);   // optimizer slots of one fit workgroup
-// k_cg_fit_g (variant 1): two single-wave workgroups per SIMD, slot records of kFitGSlotBytes in global memory
-constexpr int kFitGBlocksPerCU = 8;
-constexpr int kFitGSlotsPerWave = 128;      // = kFitGSlots (arima_fit_global.hpp, checked there)
-constexpr int kFitGSlotBytes = 512;         // >= sizeof(GSlot<K>) for every K <= 11
 // k_cg_fit workgroups are single waves (4 per CU, one per SIMD, each with a quarter of the LDS): a wave that has
 // finished its series leaves the CU at once, so the next fit's waves take its SIMD and LDS share while the other
 // waves of the CU still run their slowest series (pipelined fits)

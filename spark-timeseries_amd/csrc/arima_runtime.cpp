@@ -47,7 +47,7 @@ struct DevBuf {
 };
 
 constexpr int kNumEvents = 5;
-constexpr int kCtlWords = 32;     // device counters of the fit kernel (k_cg_fit's ctl[])
+constexpr int kCtlWords = 40;     // device counters of the fit kernel (k_cg_fit's ctl[]; ctl[32] = series written)
 
 // What arima_get_last_stats needs to turn the device counters of the last fit into arima_fit_stats. The fit
 // entry points do not wait for the device (the `*_device` contract): the counters are copied to pinned host
@@ -63,7 +63,7 @@ struct PendingStats {
 // Device workspace of one fit in flight: Hannan-Rissanen init, the fit kernel's counters and its express ring.
 struct FitWs {
     DevBuf init, hr_status, ctl, xring, xready;
-    DevBuf slots;            // k_cg_fit_g's optimizer slot records (fit_kernel = 1)
+    DevBuf rec, resp, lists, tail, mark, counts, rc;   // the rounds fit (fit_kernel = 2): records, responses, lists
 };
 
 // One lane of the order search's concurrent fits (arima_order_search_batch*): its own stream, workspace and
@@ -131,7 +131,10 @@ struct arima_handle {
     int express_blocks = -1;       // k_cg_fit express workgroups (-1: num_cus / 16)
     int express_ring = 0;          // express hand-offs per launch (0: the whole ring, sts::kExpressRingEntries)
     int hr_grid = 0;               // k_hr_init: 0 = a lane per series; > 0 = that many single-wave workgroups
-    int fit_kernel = 0;            // 0: k_cg_fit (LDS slots, 1 wave/SIMD); 1: k_cg_fit_g (global slots, 2 waves/SIMD)
+    int fit_kernel = 0;            // 0: k_cg_fit (LDS slots, 1 wave/SIMD); 2: rounds of streaming passes + k_cg_fit
+    int rounds_max = 96;           // rounds enqueued per fit (fit_kernel 2)
+    int64_t rounds_tail = -1;      // a round with at most this many requests hands them to k_cg_fit (-1: half its slots)
+    int rounds_pass_waves = 12;    // resident pass waves per CU the pass kernel's persistent grid assumes
     int64_t last_express = 0;
     int64_t last_grid = 0;
     int search_lanes = 8;          // concurrent fits of the order search (2/4/8: 1269/1303/1408 series/s, profiles/r02/g_c5)
@@ -356,6 +359,19 @@ static int check_fault(arima_handle *h, FitCtx &c) {
 
 static int take_fault(arima_handle *h);
 
+int arima_rounds_trace(arima_handle *h, unsigned *out, int max_words) {
+    if (!h || !out || max_words < 0) return ARIMA_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    HIPCHK(h, hipSetDevice(h->device));
+    if (h->stats_ctx < 0) return 0;
+    FitCtx &c = h->fctx[h->stats_ctx];
+    if (c.has_done) HIPCHK(h, hipEventSynchronize(c.ev_done));
+    if (!c.ws.rc.ptr) return 0;
+    const int words = (int)std::min<size_t>((size_t)max_words, c.ws.rc.bytes / sizeof(unsigned));
+    HIPCHK(h, hipMemcpy(out, c.ws.rc.ptr, (size_t)words * sizeof(unsigned), hipMemcpyDeviceToHost));
+    return words;
+}
+
 int arima_synchronize(arima_handle *h) {
     if (!h) return ARIMA_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
@@ -379,7 +395,17 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
     if (!h || !name) return ARIMA_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
     if (!strcmp(name, "smear")) { h->smear = value ? 1 : 0; return ARIMA_OK; }
-    if (!strcmp(name, "fit_kernel")) { h->fit_kernel = value ? 1 : 0; return ARIMA_OK; }
+    if (!strcmp(name, "fit_kernel")) {
+        if (value != 0 && value != 2) return set_err(h, ARIMA_E_INVALID_ARG, "fit_kernel: 0 or 2");
+        h->fit_kernel = (int)value;
+        return ARIMA_OK;
+    }
+    if (!strcmp(name, "rounds_max")) { h->rounds_max = (int)std::min<int64_t>(4096, std::max<int64_t>(1, value)); return ARIMA_OK; }
+    if (!strcmp(name, "rounds_tail")) { h->rounds_tail = std::max<int64_t>(-1, value); return ARIMA_OK; }
+    if (!strcmp(name, "rounds_pass_waves")) {
+        h->rounds_pass_waves = (int)std::min<int64_t>(32, std::max<int64_t>(1, value));
+        return ARIMA_OK;
+    }
     if (!strcmp(name, "hr_grid")) { h->hr_grid = (int)std::min<int64_t>(1 << 20, std::max<int64_t>(0, value)); return ARIMA_OK; }
     if (!strcmp(name, "express_ring")) {
         h->express_ring = (int)std::min<int64_t>(sts::kExpressRingEntries, std::max<int64_t>(0, value));
@@ -412,7 +438,8 @@ int arima_get_option(const arima_handle *hc, const char *name, int64_t *value) {
         {"smear", h->smear}, {"express_blocks", h->express_blocks}, {"grid_blocks", h->grid_blocks_override},
         {"search_lanes", h->search_lanes}, {"fit_pipeline", h->pipeline}, {"host_pipeline", h->host_pipeline},
         {"host_chunk", h->host_chunk}, {"fit_slice_bytes", h->fit_slice_bytes}, {"express_ring", h->express_ring},
-        {"fit_kernel", h->fit_kernel}, {"hr_grid", h->hr_grid}};
+        {"fit_kernel", h->fit_kernel}, {"hr_grid", h->hr_grid}, {"rounds_max", h->rounds_max},
+        {"rounds_tail", h->rounds_tail}, {"rounds_pass_waves", h->rounds_pass_waves}};
     for (const auto &o : opts)
         if (!strcmp(name, o.n)) {
             *value = o.v;
@@ -447,6 +474,19 @@ static hipError_t end_fit(FitCtx &c, hipStream_t s) {
     hipError_t e = hipEventRecord(c.ev_done, s);
     if (e == hipSuccess) c.has_done = true;
     return e;
+}
+
+// Workspaces of the rounds fit (fit_kernel = 2) for N series of k parameters.
+static int ensure_rounds_ws(arima_handle *h, FitWs &ws, int64_t N, int k) {
+    const int kk = std::max(1, std::min(k, 11));
+    int rc = ws.rec.ensure((size_t)N * sts::rounds_rec_bytes(kk));
+    if (rc == ARIMA_OK) rc = ws.resp.ensure((size_t)N * sts::rounds_resp_words(kk) * sizeof(double));
+    if (rc == ARIMA_OK) rc = ws.lists.ensure((size_t)2 * sts::kRoundLists * N * sizeof(int32_t));
+    if (rc == ARIMA_OK) rc = ws.tail.ensure((size_t)N * sizeof(int32_t));
+    if (rc == ARIMA_OK) rc = ws.mark.ensure((size_t)N);
+    if (rc == ARIMA_OK) rc = ws.counts.ensure((size_t)sts::rounds_ranges(N) * 8 * sizeof(unsigned));
+    if (rc == ARIMA_OK) rc = ws.rc.ensure((size_t)(h->rounds_max + 2) * sts::kRcStride * sizeof(unsigned));
+    return rc;
 }
 
 // Hannan-Rissanen init (unless user init) and the fit kernel -- or the AR-only shortcut, or a uniform per-series
@@ -500,7 +540,7 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
     int bcus = h->grid_blocks_override;
     if (bcus <= 0) bcus = std::max(1, cus - xcus);
     const int variant = h->fit_kernel;
-    const int bpc = variant == 1 ? sts::kFitGBlocksPerCU : sts::kFitBlocksPerCU;
+    const int bpc = sts::kFitBlocksPerCU;
     int xblocks = xcus * bpc;
     int blocks = bcus * bpc;
     const int per_block = std::max(1, sts::cg_fit_series_per_block(p, q, I, variant));
@@ -511,14 +551,30 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
         RCCHK(h, ws.xready.ensure(sts::kExpressReadyBytes), "workspace");
         HIPCHK(h, hipMemsetAsync(ws.xready.ptr, 0, sts::kExpressReadyBytes, s));
     }
-    if (variant == 1)
-        RCCHK(h, ws.slots.ensure((size_t)blocks * sts::kFitGSlotsPerWave * sts::kFitGSlotBytes), "workspace");
+    sts::FitRounds rounds{};
+    if (variant == 2) {
+        RCCHK(h, ensure_rounds_ws(h, ws, N, k), "workspace");
+        HIPCHK(h, hipMemsetAsync(ws.rc.ptr, 0, (size_t)(h->rounds_max + 2) * sts::kRcStride * sizeof(unsigned), s));
+        rounds.rec = ws.rec.as<unsigned char>();
+        rounds.resp = ws.resp.as<double>();
+        rounds.lists = ws.lists.as<int32_t>();
+        rounds.tail = ws.tail.as<int32_t>();
+        rounds.mark = ws.mark.as<uint8_t>();
+        rounds.counts = ws.counts.as<unsigned>();
+        rounds.rc = ws.rc.as<unsigned>();
+        rounds.max_rounds = h->rounds_max;
+        rounds.tail_at = (unsigned)std::min<int64_t>(
+            0xffffffffll, h->rounds_tail >= 0 ? h->rounds_tail : (int64_t)blocks * per_block / 2);
+        rounds.pass_blocks = cus * h->rounds_pass_waves;
+        rounds.advance_blocks = cus * 8;
+        blocks = bcus * bpc;                // the tail's size is known on the device only: the whole grid
+    }
     *grid_out = blocks;
     *express_out = xcus;                    // in CUs, the unit of the "express_blocks" option
     RCCHK(h, sts::launch_cg_fit(y, ldn, n, N, p, q, I, h->smear, init, init_status, d_coef, d_ll, d_status, d_neval,
                                 d_ngrad, d_flags, ws.ctl.as<unsigned long long>(), blocks, xblocks,
                                 ws.xring.as<unsigned char>(), ws.xready.as<unsigned>(), shared_gpu ? 0 : 1, variant,
-                                ws.slots.as<unsigned char>(), s),
+                                &rounds, s),
           "cg_fit");
     hipLaunchKernelGGL(k_fault_merge, dim3(1), dim3(64), 0, s, ws.ctl.as<unsigned long long>(),
                        h->dev_fault.as<unsigned long long>());
@@ -537,9 +593,7 @@ static int reserve_fit_ws(arima_handle *h, int count, int64_t N, int64_t ldn, in
         RCCHK(h, c.ws.ctl.ensure(kCtlWords * sizeof(unsigned long long)), "workspace");
         RCCHK(h, c.ws.xring.ensure(sts::kExpressRingBytes), "workspace");
         RCCHK(h, c.ws.xready.ensure(sts::kExpressReadyBytes), "workspace");
-        if (h->fit_kernel == 1)
-            RCCHK(h, c.ws.slots.ensure((size_t)std::max(1, h->num_cus) * sts::kFitGBlocksPerCU *
-                                       sts::kFitGSlotsPerWave * sts::kFitGSlotBytes), "workspace");
+        if (h->fit_kernel == 2) RCCHK(h, ensure_rounds_ws(h, c.ws, N, k), "workspace");
     }
     return ARIMA_OK;
 }
@@ -624,6 +678,8 @@ static arima_fit_stats compute_stats(const PendingStats &ps, const unsigned long
     st.wave_multi_passes = (int64_t)cc[8];
     st.spec_chains = (int64_t)cc[9];
     st.ride_passes = (int64_t)cc[18];
+    // series the kernels wrote; the AR-only shortcut, user-uniform statuses and an empty fit write every series
+    st.series_done = ps.cg ? (int64_t)cc[32] : N;
     st.express_series = (int64_t)cc[23];
     st.express_f_passes = (int64_t)cc[24];
     st.express_g_passes = (int64_t)cc[25];
@@ -767,6 +823,7 @@ static void acc_stats(arima_fit_stats &a, const arima_fit_stats &s) {
     a.spec_hits += s.spec_hits;
     a.spec_chains += s.spec_chains;
     a.ride_passes += s.ride_passes;
+    a.series_done += s.series_done;
     a.express_series += s.express_series;
     a.express_f_passes += s.express_f_passes;
     a.express_g_passes += s.express_g_passes;
@@ -1128,9 +1185,7 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
         if (rc == ARIMA_OK) rc = ln.ws.ctl.ensure(kCtlWords * sizeof(unsigned long long));
         if (rc == ARIMA_OK) rc = ln.ws.xring.ensure(sts::kExpressRingBytes);
         if (rc == ARIMA_OK) rc = ln.ws.xready.ensure(sts::kExpressReadyBytes);
-        if (rc == ARIMA_OK && h->fit_kernel == 1)
-            rc = ln.ws.slots.ensure((size_t)std::max(1, h->num_cus) * sts::kFitGBlocksPerCU * sts::kFitGSlotsPerWave *
-                                    sts::kFitGSlotBytes);
+        if (rc == ARIMA_OK && h->fit_kernel == 2) rc = ensure_rounds_ws(h, ln.ws, N, 11);
         if (rc != ARIMA_OK) {
             if (j == 0) return set_err(h, rc, "order search workspace");
             break;                                 // fewer lanes instead of failing the call

@@ -48,7 +48,7 @@ EXPORTED = [
     "arima_difference_batch", "arima_inverse_difference_batch", "arima_css_loglik_batch",
     "arima_css_gradient_batch", "arima_hannan_rissanen_batch", "arima_forecast_batch", "arima_model_flags_batch",
     "arima_sample_batch_device", "arima_order_search_batch", "arima_order_search_batch_device",
-    "arima_forecast_batch_device", "arima_synchronize",
+    "arima_forecast_batch_device", "arima_synchronize", "arima_rounds_trace",
 ]
 
 
@@ -62,7 +62,7 @@ class FitStats(ctypes.Structure):
                 ("express_blocks", ctypes.c_int64), ("express_series", ctypes.c_int64),
                 ("express_f_passes", ctypes.c_int64), ("express_g_passes", ctypes.c_int64),
                 ("fault", ctypes.c_int64), ("fault_info", ctypes.c_int64 * 5),
-                ("diag", ctypes.c_int64 * 6), ("ride_passes", ctypes.c_int64)]
+                ("diag", ctypes.c_int64 * 6), ("ride_passes", ctypes.c_int64), ("series_done", ctypes.c_int64)]
 
     def as_dict(self):
         d = {name: getattr(self, name) for name, _ in self._fields_}
@@ -117,6 +117,7 @@ def load():
         L.arima_get_last_stats.argtypes = [H, ctypes.POINTER(FitStats)]
         L.arima_set_option.argtypes = [H, ctypes.c_char_p, _i64]
         L.arima_get_option.argtypes = [H, ctypes.c_char_p, ctypes.POINTER(_i64)]
+        L.arima_rounds_trace.argtypes = [H, ctypes.POINTER(ctypes.c_uint), ctypes.c_int]
         L.arima_synchronize.argtypes = [H]
         L.arima_fit_batch.argtypes = [H, _dp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _dp, _dp, _dp, _i32p,
                                       _i32p, _i32p, _u8p]
@@ -189,6 +190,19 @@ class Engine:
         v = _i64()
         self._check(self.L.arima_get_option(self.h, name.encode(), ctypes.byref(v)), "arima_get_option")
         return int(v.value)
+
+    def rounds_trace(self):
+        """Round-control words of the last device fit (fit_kernel 2): an array (rounds, 8) -- counts of lists G,
+        F+2, F+1, F+0, the tile counter -- and the tail count."""
+        R = self.get_option("rounds_max")
+        buf = (ctypes.c_uint * ((R + 2) * 8))()
+        n = self.L.arima_rounds_trace(self.h, buf, (R + 2) * 8)
+        if n < 0:
+            self._check(n, "arima_rounds_trace")
+        a = np.frombuffer(buf, dtype=np.uint32)[:n].copy()
+        if a.size < (R + 2) * 8:
+            return None, None
+        return a[: R * 8].reshape(R, 8), int(a[(R + 1) * 8])
 
     def synchronize(self):
         """Wait for the device work of every call issued on this handle (the *_device calls are asynchronous)."""

@@ -169,6 +169,7 @@ def test_full_size_properties(engine):
     for k in r1:
         assert np.array_equal(r1[k][perm], r3[k], equal_nan=True), k
     assert stats["n_eval"] == int(r1["n_eval"].sum()) and stats["n_grad"] == int(r1["n_grad"].sum())
+    assert stats["series_done"] == N
     ok = r1["status"] == 0
     assert ok.mean() > 0.99
     assert np.all(np.isfinite(r1["ll"][ok]))
