@@ -366,12 +366,19 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
                             int32_t *__restrict__ status_out, int32_t *__restrict__ n_eval_out,
                             int32_t *__restrict__ n_grad_out, uint8_t *__restrict__ flags_out,
                             unsigned long long *__restrict__ ctl, unsigned char *__restrict__ xq,
-                            unsigned *__restrict__ xready, int64_t N, int lane) {
+                            unsigned *__restrict__ xready, int64_t N, int lane,
+                            const int32_t *__restrict__ direct_list = nullptr,
+                            const unsigned char *__restrict__ direct_rec = nullptr) {
+    // direct mode (direct_list != nullptr, the tail of a rounds fit): no bulk waves and no ring -- a group claims the
+    // next listed series from the work counter ctl[0] (N = the list's length) and loads its optimizer state from
+    // its record in direct_rec; up to 4 series per wave (each group needs K <= 16 lanes for the gradient columns)
     constexpr int K = I + P + Q;
     constexpr int NS = spec_ns<K>();
+    const bool direct = direct_list != nullptr;
     const int gbytes = express_group_bytes<K>(n);
     int XG = lds_bytes / gbytes;
-    XG = XG >= kExpressGroups ? kExpressGroups : (XG >= 2 ? 2 : 1);
+    if (direct) XG = XG >= 4 ? 4 : (XG >= 2 ? 2 : 1);
+    else XG = XG >= kExpressGroups ? kExpressGroups : (XG >= 2 ? 2 : 1);
     const int GL = 64 / XG;                                 // lanes per group
     const int grp = lane / GL, gl = lane % GL;
     const bool glead = gl == 0;
@@ -388,7 +395,7 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
     unsigned long long tk_time = 0, tk_polls = 0;          // fault diagnostics: this ticket's age and polls,
     unsigned tk_rfirst = 0, tk_rmax = 0;                    // first / largest ready word seen
     if (glead) {
-        ticket = add_agent(&ctl[20], 1ull);
+        ticket = add_agent(direct ? &ctl[0] : &ctl[20], 1ull);
         tk_time = __builtin_amdgcn_s_memrealtime();
     }
     ticket = __shfl(ticket, grp * GL);
@@ -396,7 +403,9 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
     for (;;) {
         // ---- groups waiting on a ticket: poll (group leader), then load the entry (whole group) ----
         int arrived = 0;
-        if (gstate == 0 && glead) {
+        if (direct) {
+            if (gstate == 0) arrived = ticket < (unsigned long long)N ? 1 : 2;
+        } else if (gstate == 0 && glead) {
             const unsigned e = (unsigned)(ticket % xring);
             const unsigned long long *ent = reinterpret_cast<const unsigned long long *>(xq + (size_t)e * kExpressEntryBytes);
             // poll the ready word; every 32nd poll reads it at the memory side
@@ -444,7 +453,16 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
         arrived = __shfl(arrived, grp * GL);
         if (arrived == 2) gstate = 2;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (arrived == 1) {
+        if (arrived == 1 && direct) {
+            using DLane = CGLane<K, NS, spec_nc<K>()>;
+            const int64_t dsid = direct_list[ticket];
+            const unsigned long long *src = reinterpret_cast<const unsigned long long *>(
+                direct_rec + dsid * (int64_t)((sizeof(DLane) + 127) / 128 * 128));
+            constexpr int W = (int)(sizeof(DLane) / 8);
+            static_assert(sizeof(DLane) % 8 == 0, "8-byte words");
+            for (int w = gl; w < W; w += GL) reinterpret_cast<unsigned long long *>(&ES.s)[w] = src[w];
+            if (glead) ES.sid = dsid;
+        } else if (arrived == 1) {
             const unsigned e = (unsigned)(ticket % xring);
             const unsigned long long *src = reinterpret_cast<const unsigned long long *>(xq + (size_t)e * kExpressEntryBytes);
             constexpr int W = (int)(sizeof(FitSlotCore<K>) / 8);
@@ -519,7 +537,7 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
             grads += ES.s.n_grad;
             hits += ES.s.spec_hits;
             done++;
-            ticket = add_agent(&ctl[20], 1ull);
+            ticket = add_agent(direct ? &ctl[0] : &ctl[20], 1ull);
             tk_time = __builtin_amdgcn_s_memrealtime();
             tk_polls = 0;
             tk_rfirst = tk_rmax = 0;
@@ -565,6 +583,12 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const bool has_express = n_bulk < (int)gridDim.x;
     if (resume_list) N = (int64_t)*resume_n;             // written by the previous kernel (stream order)
+    if (resume_list && n_bulk == 0) {                     // the tail of a rounds fit, every wave on the express path
+        fit_express<P, Q, I, SMEAR>(reinterpret_cast<unsigned char *>(&slots[wave][0]), (int)sizeof(slots[0]), y, ld,
+                                    n, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out, ctl, xq,
+                                    xready, N, lane, resume_list, resume_rec);
+        return;
+    }
     if ((int)blockIdx.x >= n_bulk) {                      // express workgroup: this wave's share of the LDS
         fit_express<P, Q, I, SMEAR>(reinterpret_cast<unsigned char *>(&slots[wave][0]), (int)sizeof(slots[0]), y, ld,
                                     n, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out, ctl, xq,
@@ -1114,6 +1138,11 @@ int launch_cg_fit_PS(const double *y, int64_t ld, int n, int64_t N, int q, int I
                         resume_list = R.tail;
                         resume_n = tail_n;
                         resume_rec = R.rec;
+                        if (R.tail_express && n <= express_max_n<K>(lds_per_wave)) {
+                            // every workgroup an express wave claiming tail series directly (no bulk, no ring)
+                            express_blocks += grid_blocks;
+                            grid_blocks = 0;
+                        }
                     }
                     hipLaunchKernelGGL((k_cg_fit<P, Q, II, S, SPW>), dim3(grid_blocks + express_blocks),
                                        dim3(64 * kFitWaves), 0, s, y, ld, n, N, init, init_status, coef_out, ll_out,

@@ -38,6 +38,7 @@ struct FitRounds {
     int max_rounds;                // rounds enqueued (the last one hands every unfinished series to k_cg_fit)
     unsigned tail_at;              // a round with at most this many requests hands them to k_cg_fit
     int pass_blocks, advance_blocks;   // persistent grids (single-wave workgroups)
+    int tail_express;              // 1: the tail runs on express waves only (a wave per series, rows in LDS)
 };
 int rounds_rec_bytes(int k);       // record stride of k parameters (a multiple of 128 B)
 int rounds_resp_words(int k);

@@ -91,7 +91,7 @@ struct SliceSlot {
 
 constexpr int kMaxSearchLanes = 8;
 constexpr int kMaxD = 16;
-constexpr int kMaxPipeline = 4;
+constexpr int kMaxPipeline = 8;
 
 // One fit context: what a fit call needs for itself (stream, differenced-series workspace, HR init, kernel counters,
 // timing events, pinned counter copy, host-path staging). Fit calls rotate over h->pipeline contexts, so with
@@ -135,6 +135,9 @@ struct arima_handle {
     int rounds_max = 96;           // rounds enqueued per fit (fit_kernel 2)
     int64_t rounds_tail = -1;      // a round with at most this many requests hands them to k_cg_fit (-1: half its slots)
     int rounds_pass_waves = 12;    // resident pass waves per CU the pass kernel's persistent grid assumes
+    int rounds_tail_express = 0;   // the rounds' tail on express waves only (1) or on k_cg_fit's bulk + express (0)
+    int rounds_tail_cus = 0;       // k_cg_fit grid of the rounds' tail: bulk CUs (0: all), express CUs (-1: default)
+    int rounds_tail_xcus = -1;
     int64_t last_express = 0;
     int64_t last_grid = 0;
     int search_lanes = 8;          // concurrent fits of the order search (2/4/8: 1269/1303/1408 series/s, profiles/r02/g_c5)
@@ -401,6 +404,9 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
         return ARIMA_OK;
     }
     if (!strcmp(name, "rounds_max")) { h->rounds_max = (int)std::min<int64_t>(4096, std::max<int64_t>(1, value)); return ARIMA_OK; }
+    if (!strcmp(name, "rounds_tail_express")) { h->rounds_tail_express = value ? 1 : 0; return ARIMA_OK; }
+    if (!strcmp(name, "rounds_tail_cus")) { h->rounds_tail_cus = (int)std::max<int64_t>(0, value); return ARIMA_OK; }
+    if (!strcmp(name, "rounds_tail_xcus")) { h->rounds_tail_xcus = (int)std::max<int64_t>(-1, value); return ARIMA_OK; }
     if (!strcmp(name, "rounds_tail")) { h->rounds_tail = std::max<int64_t>(-1, value); return ARIMA_OK; }
     if (!strcmp(name, "rounds_pass_waves")) {
         h->rounds_pass_waves = (int)std::min<int64_t>(32, std::max<int64_t>(1, value));
@@ -439,7 +445,9 @@ int arima_get_option(const arima_handle *hc, const char *name, int64_t *value) {
         {"search_lanes", h->search_lanes}, {"fit_pipeline", h->pipeline}, {"host_pipeline", h->host_pipeline},
         {"host_chunk", h->host_chunk}, {"fit_slice_bytes", h->fit_slice_bytes}, {"express_ring", h->express_ring},
         {"fit_kernel", h->fit_kernel}, {"hr_grid", h->hr_grid}, {"rounds_max", h->rounds_max},
-        {"rounds_tail", h->rounds_tail}, {"rounds_pass_waves", h->rounds_pass_waves}};
+        {"rounds_tail", h->rounds_tail}, {"rounds_pass_waves", h->rounds_pass_waves},
+        {"rounds_tail_express", h->rounds_tail_express}, {"rounds_tail_cus", h->rounds_tail_cus},
+        {"rounds_tail_xcus", h->rounds_tail_xcus}};
     for (const auto &o : opts)
         if (!strcmp(name, o.n)) {
             *value = o.v;
@@ -567,7 +575,12 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
             0xffffffffll, h->rounds_tail >= 0 ? h->rounds_tail : (int64_t)blocks * per_block / 2);
         rounds.pass_blocks = cus * h->rounds_pass_waves;
         rounds.advance_blocks = cus * 8;
-        blocks = bcus * bpc;                // the tail's size is known on the device only: the whole grid
+        rounds.tail_express = h->rounds_tail_express;
+        // the tail's size is known on the device only: a grid of rounds_tail_cus CUs' worth of bulk workgroups
+        // (<= 0: all), rounds_tail_xcus of express ones (< 0: as a plain fit)
+        blocks = (h->rounds_tail_cus > 0 ? std::min(bcus, h->rounds_tail_cus) : bcus) * bpc;
+        if (h->rounds_tail_xcus >= 0) xblocks = std::min(h->rounds_tail_xcus, cus) * bpc;
+        if (blocks + xblocks == 0) blocks = bpc;
     }
     *grid_out = blocks;
     *express_out = xcus;                    // in CUs, the unit of the "express_blocks" option
