@@ -77,9 +77,9 @@ struct SearchLane {
     DevBuf coef, ll, status, neval, ngrad, flags;
 };
 
-// A device fit larger than one slice (option "fit_slice_bytes" of differenced workspace, default 8 GiB = 1M series of
-// T = 1024) runs as consecutive slices over the fit contexts: the workspaces stay bounded whatever the batch (C3's 8M
-// series on one GPU), and the slices pipeline like consecutive calls. Every slice takes the next slot of a ring with
+// A device fit larger than one slice (option "fit_slice_bytes" of differenced workspace; default 0 = 60 % of the free
+// HBM over the fit contexts) runs as consecutive slices over the fit contexts: the workspaces stay bounded whatever
+// the batch (C3's 8M series on one GPU), and the slices pipeline like consecutive calls. Every slice takes the next slot of a ring with
 // its own timing events and its own pinned copy of the kernel counters, so the call's stats cover every slice. A
 // slot is reused only once its previous slice's copy has landed (host check on its last event).
 constexpr int kSliceSlots = 64;
@@ -144,7 +144,7 @@ struct arima_handle {
     int pipeline = 1;              // fit contexts in rotation (option "fit_pipeline")
     int host_pipeline = 3;         // contexts the chunked host path rotates over
     int64_t host_chunk = 1 << 18;  // series per chunk of the host path (option "host_chunk")
-    int64_t fit_slice_bytes = 8ll << 30;   // differenced workspace of one device-fit slice (option "fit_slice_bytes")
+    int64_t fit_slice_bytes = 0;   // differenced workspace of one device-fit slice (option "fit_slice_bytes"; 0: from free HBM)
     SliceSlot slot[kSliceSlots];
     unsigned long long *slot_ctl = nullptr;     // pinned, kCtlWords per slot
     unsigned slot_seq = 0;                      // slots taken so far
@@ -432,7 +432,7 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
         return ARIMA_OK;
     }
     if (!strcmp(name, "host_chunk")) { h->host_chunk = std::max<int64_t>(1, value); return ARIMA_OK; }
-    if (!strcmp(name, "fit_slice_bytes")) { h->fit_slice_bytes = std::max<int64_t>(1, value); return ARIMA_OK; }
+    if (!strcmp(name, "fit_slice_bytes")) { h->fit_slice_bytes = std::max<int64_t>(0, value); return ARIMA_OK; }
     return set_err(h, ARIMA_E_INVALID_ARG, "unknown option");
 }
 
@@ -743,7 +743,18 @@ int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_se
     const int P = h->pipeline;
     HIPCHK(h, hipSetDevice(h->device));
     const int64_t ldn = round_up(std::max(T - d, 1), 16);
-    const int64_t slice = std::max<int64_t>(1024, h->fit_slice_bytes / (ldn * (int64_t)sizeof(double)) / 1024 * 1024);
+    // Slice size: option fit_slice_bytes, or (0, the default) as large as the free HBM allows for P contexts. Every
+    // slice ends with its own slowest series (the launch's critical path), so fewer, larger slices are faster (C4 at
+    // 1M x 4096 in 262k-series slices: 2.9 s per fit alone, one slice: 1.2 s).
+    int64_t slice_bytes = h->fit_slice_bytes;
+    if (slice_bytes <= 0) {
+        size_t free_b = 0, total_b = 0;
+        HIPCHK(h, hipMemGetInfo(&free_b, &total_b));
+        size_t held = 0;                           // the contexts' differenced workspaces are reused
+        for (int j = 0; j < P; ++j) held += h->fctx[j].diff.bytes;
+        slice_bytes = std::max<int64_t>(1ll << 30, (int64_t)((free_b + held) / 10 * 6 / (size_t)std::max(P, 1)));
+    }
+    const int64_t slice = std::max<int64_t>(1024, slice_bytes / (ldn * (int64_t)sizeof(double)) / 1024 * 1024);
     if (n_series <= slice || T < 0 || ld < T || n_series < 0) {
         const int ci = (int)(h->fit_seq++ % (unsigned)P);
         FitCtx &c = h->fctx[ci];

@@ -555,7 +555,7 @@ def test_sliced_device_fit_matches_unsliced(engine, pipeline):
     try:
         sliced, st = run()
     finally:
-        engine.set_option("fit_slice_bytes", 8 << 30)
+        engine.set_option("fit_slice_bytes", 0)
         engine.set_option("fit_pipeline", 1)
     for x, y in zip(whole, sliced):
         assert _same(x, y)
