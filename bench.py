@@ -13,7 +13,7 @@ collective; gloo carries only the timing barrier and the max-over-ranks reductio
   --series S        series per GPU (weak scaling, default 1M: configs[1], and configs[2] read per GPU)
   --total-series S  fixed total over all GPUs (strong scaling: configs[2] = 8M series sharded over N GPUs)
   --smear 0|1       Breeze overlap reading at ARIMA.scala:526 (default 1)
-  --pipeline P      fit contexts in rotation (arima_set_option "fit_pipeline", default 3): step i+1's differencing,
+  --pipeline P      fit contexts in rotation (arima_set_option "fit_pipeline", default 6; 4 for c4): step i+1's differencing,
                     init and bulk fit run while step i's slowest series finish; every step is still a
                     complete fit of every series, into its own output buffers (one set per context)
   --e2e 0|1         also time one arima_fit_batch call from pageable host memory (default 1)
@@ -30,6 +30,14 @@ import socket
 import subprocess
 import sys
 import time
+
+# Each fit context (and each order-search lane) is its own HIP stream. HIP maps a process's streams onto
+# GPU_MAX_HW_QUEUES hardware queues (default 4), and kernels of streams that share a queue run one after the other:
+# 6 contexts + the handle's stream need 8 queues to overlap (C2: 8.65 M series/s with 4 queues and 3 contexts,
+# 9.5-9.7 with 8-16 queues and 6-8 contexts; C5's 8 search lanes: 4638 -> 5497 series/s; profiles/r03/j_hwq/{a,b}).
+# Set before anything initialises HIP (the GPU boxes export 4); a larger setting in the environment is kept.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or "4") < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "spark-timeseries_amd"))
@@ -195,7 +203,8 @@ def main():
     ap.add_argument("--smear", type=int, default=1, choices=[0, 1])
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (0 = skip)")
     ap.add_argument("--grid-blocks", type=int, default=0)
-    ap.add_argument("--pipeline", type=int, default=3)
+    ap.add_argument("--pipeline", type=int, default=0,
+                    help="fit contexts (0: 6, or 4 for c4, whose 1M x 4096 fit then stays one slice of free HBM)")
     ap.add_argument("--express-blocks", type=int, default=-1, help="express workgroups of the fit kernel (-1: CUs/16)")
     ap.add_argument("--e2e", type=int, default=1, choices=[0, 1])
     ap.add_argument("--fit-kernel", type=int, default=-1, help="0: k_cg_fit (LDS slots), 2: rounds of streaming passes; -1: default")
@@ -227,6 +236,8 @@ def main():
         dist.init_process_group("gloo")
 
     p, d, q, I, T, base, jitter = CONFIGS[args.config]
+    if args.pipeline <= 0:
+        args.pipeline = 4 if args.config == "c4" else 6
     if args.config == "c5" and not args.total_series:
         args.total_series = 1 << 20                 # configs[4]: 1M series over the node's GPUs
     if args.total_series:
