@@ -96,6 +96,10 @@ __global__ __launch_bounds__(256) void k_inverse_difference(const double *__rest
 // indices no later step can touch (< tile end - d: index x is written at step x or x + d) leave as coalesced
 // row segments. [T-d, T + nFuture) (the diffMatrix diagonal, the forecasts and their re-integration, ≤ 3 % of
 // the bytes) is written by the lane itself, as before.
+// Tiles are phase-shifted by d (round 3): tile k covers steps [d + (k-1) kFcCh, d + k kFcCh), so after it exactly the
+// outputs below k kFcCh are final and every flush is a whole kFcCh-element segment at a kFcCh boundary -- with a
+// 128-B aligned output row stride (ld_out % 16 == 0) each one is two full 128-B lines per row instead of a segment
+// straddling three (the round-2 kernel wrote 1.18x its output bytes).
 // =======================================================================================================
 constexpr int kFcMaxOrder = 5;   // p, q <= 5 (check_orders)
 constexpr int kFcMaxD = 8;
@@ -162,7 +166,8 @@ __global__ __launch_bounds__(kFcWave) void k_forecast(const double *__restrict__
     const int tu = lane % kFcCh, tr = lane / kFcCh;
     double pf[kFcCh];
     auto load_tile = [&](int cb) {
-        const int t = cb + tu < T ? cb + tu : T - 1;
+        const int tt = cb + tu < T ? cb + tu : T - 1;
+        const int t = tt < 0 ? 0 : tt;                                 // the first tile starts before t = 0
 #pragma unroll
         for (int j = 0; j < kFcCh; ++j) {
             const int64_t gi = row0 + j * kFcRowsPerLd + tr;
@@ -174,16 +179,19 @@ __global__ __launch_bounds__(kFcWave) void k_forecast(const double *__restrict__
         }
     };
     int flushed = 0;                                                   // [0, flushed) is in HBM
-    if (T > 0) load_tile(0);
-    for (int cb = 0; cb < T; cb += kFcCh) {
+    const int cb0 = d - kFcCh;                                         // first tile: steps [0, d)
+    if (T > 0) load_tile(cb0);
+    for (int cb = cb0; cb < T; cb += kFcCh) {
         __syncthreads();                                               // last tile's reads and flush done
+        if (cb + tu >= 0) {
 #pragma unroll
-        for (int j = 0; j < kFcCh; ++j) ring[j * kFcRowsPerLd + tr][(cb + tu) % kFcRing] = pf[j];
+            for (int j = 0; j < kFcCh; ++j) ring[j * kFcRowsPerLd + tr][(cb + tu) % kFcRing] = pf[j];
+        }
         __syncthreads();
         if (cb + kFcCh < T) load_tile(cb + kFcCh);
         const int ce = cb + kFcCh < T ? cb + kFcCh : T;
 #pragma unroll 1
-        for (int t = cb; t < ce; ++t) {
+        for (int t = cb < 0 ? 0 : cb; t < ce; ++t) {
             const double v = ring[lane][t % kFcRing];
             // differencing column t (UnivariateTimeSeries.scala:384-405 pass r: out(t) = in(t) - in(t-1) for t >= r)
             Dc[0] = v;
@@ -330,6 +338,12 @@ __global__ __launch_bounds__(256) void k_search_init(double *__restrict__ best_a
     for (int j = 0; j < kSearchK; ++j) coef[i * kSearchK + j] = __builtin_nan("");
 }
 
+// position of (p, d, q, I) in the grid's (d, p, q, intercept) order; an empty best (order -1) sorts last
+__device__ __forceinline__ int search_key(int p, int d, int q, int I) { return ((d * 16 + p) * 16 + q) * 2 + I; }
+__device__ __forceinline__ int search_key(const int32_t *o) {
+    return o[0] < 0 ? 0x7fffffff : search_key(o[0], o[1], o[2], o[3]);
+}
+
 __global__ __launch_bounds__(256) void k_search_select(const double *__restrict__ cand_coef,
                                                        const double *__restrict__ cand_ll,
                                                        const int32_t *__restrict__ cand_status,
@@ -347,13 +361,49 @@ __global__ __launch_bounds__(256) void k_search_select(const double *__restrict_
         return;
     const int k = I + p + q;
     const double aic = -2.0 * cand_ll[i] + (double)(2 * k);
-    if (!(aic < best_aic[i])) return;
+    // the first minimum in (d, p, q, intercept) order wins (minBy), whatever order the candidates arrive in
+    const double b = best_aic[i];
+    if (!(aic < b) && !(aic == b && search_key(p, d, q, I) < search_key(order + i * 4))) return;
     best_aic[i] = aic;
     order[i * 4 + 0] = p;
     order[i * 4 + 1] = d;
     order[i * 4 + 2] = q;
     order[i * 4 + 3] = I;
     for (int j = 0; j < kSearchK; ++j) coef[i * kSearchK + j] = j < k ? cand_coef[i * k + j] : 0.0;
+}
+
+// the lanes' bests -> the call's outputs, by the same rule (approxAIC, then grid position)
+__global__ __launch_bounds__(256) void k_search_merge(const SearchBests b, int lanes, int64_t N,
+                                                      double *__restrict__ best_aic, int32_t *__restrict__ order,
+                                                      double *__restrict__ coef) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    int w = -1;
+    double wa = __builtin_inf();
+    int wk = 0x7fffffff;
+    for (int l = 0; l < lanes; ++l) {
+        const int32_t *o = b.order[l] + i * 4;
+        if (o[0] < 0) continue;
+        const double a = b.aic[l][i];
+        const int key = search_key(o);
+        if (w < 0 || a < wa || (a == wa && key < wk)) {
+            w = l;
+            wa = a;
+            wk = key;
+        }
+    }
+    best_aic[i] = w < 0 ? __builtin_inf() : wa;
+    for (int j = 0; j < 4; ++j) order[i * 4 + j] = w < 0 ? -1 : b.order[w][i * 4 + j];
+    for (int j = 0; j < kSearchK; ++j) coef[i * kSearchK + j] = w < 0 ? __builtin_nan("") : b.coef[w][i * kSearchK + j];
+}
+
+int launch_search_merge(const SearchBests &b, int lanes, int64_t N, double *best_aic, int32_t *order, double *coef,
+                        hipStream_t s) {
+    if (N == 0) return ARIMA_OK;
+    if (lanes < 1 || lanes > kSearchMaxLanes) return ARIMA_E_INVALID_ARG;
+    hipLaunchKernelGGL(k_search_merge, dim3(grid_for(N, 256)), dim3(256), 0, s, b, lanes, N, best_aic, order, coef);
+    STS_CHECK_LAUNCH();
+    return ARIMA_OK;
 }
 
 int launch_search_init(double *best_aic, int32_t *order, double *coef, int64_t N, hipStream_t s) {

@@ -9,6 +9,14 @@ namespace sts {
 int launch_difference(const double *in, int64_t ld_in, double *out, int64_t ld_out, int64_t N, int T, int d,
                       int drop, hipStream_t s);
 int launch_search_init(double *best_aic, int32_t *order, double *coef, int64_t N, hipStream_t s);
+constexpr int kSearchMaxLanes = 8;
+struct SearchBests {               // the order search's per-lane best candidates (by value into k_search_merge)
+    const double *aic[kSearchMaxLanes];
+    const int32_t *order[kSearchMaxLanes];
+    const double *coef[kSearchMaxLanes];
+};
+int launch_search_merge(const SearchBests &b, int lanes, int64_t N, double *best_aic, int32_t *order, double *coef,
+                        hipStream_t s);
 int launch_search_select(const double *cand_coef, const double *cand_ll, const int32_t *cand_status,
                          const uint8_t *cand_flags, int64_t N, int p, int d, int q, int I,
                          const unsigned long long *fit_ctl, double *best_aic, int32_t *order, double *coef,

@@ -75,6 +75,7 @@ struct SearchLane {
     bool sel_recorded = false;
     FitWs ws;
     DevBuf coef, ll, status, neval, ngrad, flags;
+    DevBuf best_aic, best_order, best_coef;    // this lane's best candidate per series (merged at the end)
 };
 
 // A device fit larger than one slice (option "fit_slice_bytes" of differenced workspace; default 0 = 60 % of the free
@@ -89,7 +90,7 @@ struct SliceSlot {
     PendingStats ps;
 };
 
-constexpr int kMaxSearchLanes = 8;
+constexpr int kMaxSearchLanes = sts::kSearchMaxLanes;
 constexpr int kMaxD = 16;
 constexpr int kMaxPipeline = 8;
 
@@ -1166,6 +1167,15 @@ int arima_forecast_batch_device(arima_handle *h, const double *d_series, int64_t
 // ---------------------------------------------------------------------------------------------------------
 // order search over (d, p, q, intercept) — SURVEY.md 8(f) row 2 (config C5)
 // ---------------------------------------------------------------------------------------------------------
+// stream s waits for everything the first L search lanes have been given so far
+static void join_lanes_into(arima_handle *h, hipStream_t s, int L) {
+    for (int j = 0; j < L; ++j) {
+        SearchLane &ln = h->lanes[j];
+        if (!ln.stream) continue;
+        if (hipEventRecord(ln.ev_fit, ln.stream) == hipSuccess) hipStreamWaitEvent(s, ln.ev_fit, 0);
+    }
+}
+
 static int order_search_locked(arima_handle *h, const double *d_series, int64_t N, int32_t T, int64_t ld,
                                int32_t max_p, int32_t max_d, int32_t max_q, int32_t intercept_mode, int32_t method,
                                int32_t *d_order, double *d_coef, double *d_aic, int64_t *n_fits, hipStream_t s) {
@@ -1182,7 +1192,8 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
     // d once every fit of the previous d has finished (max_d up to 16 would not fit).
     size_t diff_bytes = 0;
     for (int d = 0; d <= max_d; ++d) diff_bytes += (size_t)N * round_up(std::max(T - d, 1), 16) * sizeof(double);
-    const size_t lane_bytes = (size_t)N * (11 * 8 * 2 + 8 + 4 * 4 + 1) + sts::kExpressRingBytes + sts::kExpressReadyBytes;
+    const size_t lane_bytes = (size_t)N * (11 * 8 * 2 + 8 + 4 * 4 + 1 + 8 + 16 + 88) + sts::kExpressRingBytes +
+                              sts::kExpressReadyBytes;
     size_t free_b = 0, total_b = 0;
     HIPCHK(h, hipMemGetInfo(&free_b, &total_b));
     size_t held = 0;                               // what this handle's search workspaces already hold
@@ -1206,6 +1217,9 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
         for (DevBuf *b : {&ln.status, &ln.neval, &ln.ngrad, &ln.ws.hr_status})
             if (rc == ARIMA_OK) rc = b->ensure((size_t)N * sizeof(int32_t));
         if (rc == ARIMA_OK) rc = ln.flags.ensure((size_t)N);
+        if (rc == ARIMA_OK) rc = ln.best_aic.ensure((size_t)N * sizeof(double));
+        if (rc == ARIMA_OK) rc = ln.best_order.ensure((size_t)N * 4 * sizeof(int32_t));
+        if (rc == ARIMA_OK) rc = ln.best_coef.ensure((size_t)N * 11 * sizeof(double));
         if (rc == ARIMA_OK) rc = ln.ws.ctl.ensure(kCtlWords * sizeof(unsigned long long));
         if (rc == ARIMA_OK) rc = ln.ws.xring.ensure(sts::kExpressRingBytes);
         if (rc == ARIMA_OK) rc = ln.ws.xready.ensure(sts::kExpressReadyBytes);
@@ -1223,7 +1237,6 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
         RCCHK(h, h->os_diff[0].ensure((size_t)N * round_up(std::max(T, 1), 16) * sizeof(double)), "workspace");
     }
     HIPCHK(h, hipEventRecord(h->ev[0], s));
-    RCCHK(h, sts::launch_search_init(d_aic, d_order, d_coef, N, s), "search_init");
     auto diff_into = [&](int d, DevBuf &buf) -> int {
         const int n = std::max(T - d, 0);
         const int64_t ldn = round_up(std::max(n, 1), 16);
@@ -1234,41 +1247,85 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
     };
     if (per_d)                                     // differencesOfOrderD once per d (ARIMA.scala:88)
         for (int d = 0; d <= max_d; ++d) RCCHK(h, diff_into(d, h->os_diff[d]), "difference");
+    // Every lane keeps its own best candidate per series, and candidates compare by (approxAIC, grid position), so
+    // the result does not depend on the order the grid points finish in: each lane runs its grid points back to back
+    // without waiting for the others (a lane's long fit no longer holds the other lanes' next fits). With one
+    // differenced copy per d the grid points go to the lanes by estimated cost, longest first (LPT); with the shared
+    // copy they keep the (d, p, q, intercept) order and the lanes join before the copy is rewritten.
+    for (int j = 0; j < L; ++j) {
+        SearchLane &ln = h->lanes[j];
+        HIPCHK(h, hipStreamWaitEvent(ln.stream, h->ev[0], 0));
+        RCCHK(h, sts::launch_search_init(ln.best_aic.as<double>(), ln.best_order.as<int32_t>(),
+                                         ln.best_coef.as<double>(), N, ln.stream), "search_init");
+    }
     const int i_lo = intercept_mode == 1 ? 1 : 0, i_hi = intercept_mode == 0 ? 0 : 1;
-    int64_t fits = 0;
-    for (int d = 0; d <= max_d; ++d) {
-        const int n = std::max(T - d, 0);
-        const int64_t ldn = round_up(std::max(n, 1), 16);
-        DevBuf &dbuf = per_d ? h->os_diff[d] : h->os_diff[0];
-        // shared copy: s has already waited (through the selects) for every fit of d - 1, the copy's readers
-        if (!per_d) RCCHK(h, diff_into(d, dbuf), "difference");
+    struct GridPoint { int d, p, q, I; double cost; };
+    std::vector<GridPoint> grid;
+    for (int d = 0; d <= max_d; ++d)
         for (int p = 0; p <= max_p; ++p)
             for (int q = 0; q <= max_q; ++q)
-                for (int I = i_lo; I <= i_hi; ++I) {
-                    // ARIMA(0,d,0) without intercept has no parameters: the reference throws (NoDataException);
-                    // fit_kernels reports it per series and the select step skips it.
-                    SearchLane &ln = h->lanes[fits % L];
-                    HIPCHK(h, hipStreamWaitEvent(ln.stream, h->ev_diff[d], 0));
-                    if (ln.sel_recorded) HIPCHK(h, hipStreamWaitEvent(ln.stream, ln.ev_sel, 0));  // outputs read
-                    int64_t grid = 0, xb = 0;
-                    RCCHK(h, fit_kernels(h, ln.ws, dbuf.as<double>(), ldn, n, N, p, q, I, method, nullptr,
-                                         ln.coef.as<double>(), ln.ll.as<double>(), ln.status.as<int32_t>(),
-                                         ln.neval.as<int32_t>(), ln.ngrad.as<int32_t>(), ln.flags.as<uint8_t>(),
-                                         ln.stream, nullptr, &grid, &xb, L > 1), "fit");
-                    HIPCHK(h, hipEventRecord(ln.ev_fit, ln.stream));
-                    // candidates are merged in grid order on the call's stream (first minimum wins, as minBy); a
-                    // fit whose kernel recorded a watchdog fault contributes nothing (its outputs are incomplete)
-                    // and the fault reaches the caller through the handle's sticky record (arima_synchronize)
-                    HIPCHK(h, hipStreamWaitEvent(s, ln.ev_fit, 0));
-                    RCCHK(h, sts::launch_search_select(ln.coef.as<double>(), ln.ll.as<double>(),
-                                                       ln.status.as<int32_t>(), ln.flags.as<uint8_t>(), N, p, d, q, I,
-                                                       ln.ws.ctl.as<unsigned long long>(), d_aic, d_order, d_coef, s),
-                          "search_select");
-                    HIPCHK(h, hipEventRecord(ln.ev_sel, s));
-                    ln.sel_recorded = true;
-                    ++fits;
-                }
+                for (int I = i_lo; I <= i_hi; ++I)
+                    // ms per 65 536 series in profiles/r03/b_c3_c5/grid_65536.jsonl follow (1+p)(1+q) (corr. 0.8);
+                    // AR-only fits (q = 0) are a single OLS
+                    grid.push_back({d, p, q, I, q == 0 ? 0.1 : (double)(1 + p) * (1 + q)});
+    std::vector<std::vector<int>> plan(L);
+    if (per_d) {
+        std::vector<int> idx(grid.size());
+        for (size_t g = 0; g < grid.size(); ++g) idx[g] = (int)g;
+        std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return grid[a].cost > grid[b].cost; });
+        std::vector<double> load(L, 0.0);
+        for (int g : idx) {
+            const int j = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+            plan[j].push_back(g);
+            load[j] += grid[g].cost;
+        }
+    } else {
+        for (size_t g = 0; g < grid.size(); ++g) plan[g % L].push_back((int)g);
     }
+    int64_t fits = 0;
+    // the shared differenced copy: the fits of one d at a time (plan order is d-major on every lane)
+    for (int dd = 0; dd <= (per_d ? 0 : max_d); ++dd) {
+        if (!per_d) {
+            if (dd > 0) join_lanes_into(h, s, L);   // every fit of d - 1 has read the copy
+            RCCHK(h, diff_into(dd, h->os_diff[0]), "difference");
+        }
+        for (int j = 0; j < L; ++j) {
+            SearchLane &ln = h->lanes[j];
+            for (int g : plan[j]) {
+                const GridPoint &gp = grid[g];
+                if (!per_d && gp.d != dd) continue;
+                const int d = gp.d, p = gp.p, q = gp.q, I = gp.I;
+                const int n = std::max(T - d, 0);
+                const int64_t ldn = round_up(std::max(n, 1), 16);
+                DevBuf &dbuf = per_d ? h->os_diff[d] : h->os_diff[0];
+                HIPCHK(h, hipStreamWaitEvent(ln.stream, h->ev_diff[d], 0));
+                // ARIMA(0,d,0) without intercept has no parameters: the reference throws (NoDataException);
+                // fit_kernels reports it per series and the select step skips it.
+                int64_t gridb = 0, xb = 0;
+                RCCHK(h, fit_kernels(h, ln.ws, dbuf.as<double>(), ldn, n, N, p, q, I, method, nullptr,
+                                     ln.coef.as<double>(), ln.ll.as<double>(), ln.status.as<int32_t>(),
+                                     ln.neval.as<int32_t>(), ln.ngrad.as<int32_t>(), ln.flags.as<uint8_t>(), ln.stream,
+                                     nullptr, &gridb, &xb, L > 1), "fit");
+                // a fit whose kernel recorded a watchdog fault contributes nothing (its outputs are incomplete) and
+                // the fault reaches the caller through the handle's sticky record (arima_synchronize)
+                RCCHK(h, sts::launch_search_select(ln.coef.as<double>(), ln.ll.as<double>(), ln.status.as<int32_t>(),
+                                                   ln.flags.as<uint8_t>(), N, p, d, q, I,
+                                                   ln.ws.ctl.as<unsigned long long>(), ln.best_aic.as<double>(),
+                                                   ln.best_order.as<int32_t>(), ln.best_coef.as<double>(),
+                                                   ln.stream),
+                      "search_select");
+                ++fits;
+            }
+        }
+    }
+    join_lanes_into(h, s, L);
+    sts::SearchBests bests{};
+    for (int j = 0; j < L; ++j) {
+        bests.aic[j] = h->lanes[j].best_aic.as<double>();
+        bests.order[j] = h->lanes[j].best_order.as<int32_t>();
+        bests.coef[j] = h->lanes[j].best_coef.as<double>();
+    }
+    RCCHK(h, sts::launch_search_merge(bests, L, N, d_aic, d_order, d_coef, s), "search_merge");
     HIPCHK(h, hipEventRecord(h->ev[3], s));
     if (n_fits) *n_fits = fits;
     return ARIMA_OK;
