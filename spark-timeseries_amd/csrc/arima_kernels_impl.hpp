@@ -216,6 +216,7 @@ constexpr bool kFRide = STS_F_RIDE != 0;     // objective requests fill the idle
 #define STS_OLD_EVALS 128
 #endif
 constexpr int kOldEvals = STS_OLD_EVALS;     // evaluations after which a series is served with priority
+
 constexpr int kFitLdsBudget = 160 * 1024 - 1024;
 // slots per wave: as many as the LDS holds, at most 2 per lane, a multiple of 8 (at least 64 unless more than
 // one wave per SIMD shares the LDS)
@@ -712,6 +713,8 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
             nOG += __popcll(mG[j] & mO[j]);
         }
         if (nF + nG == 0) break;                  // batch drained and every slot of this wave finished
+        // (round 3: a cost-aware choice -- G when min(64, nG + nF) per gradient-pass cost beats min(64, nF) per
+        // objective-pass cost -- measured at weights 2-4: C2 and C4 unchanged within noise, profiles/r03/o_gw)
         const bool doG = nOG != nOF ? nOG > nOF : (nG >= 64 || (nF < 64 && nG >= nF));
         const int rot = (int)(round_no * 37u) & 63;
         round_no++;
