@@ -35,9 +35,14 @@ import time
 # GPU_MAX_HW_QUEUES hardware queues (default 4), and kernels of streams that share a queue run one after the other:
 # 6 contexts + the handle's stream need 8 queues to overlap (C2: 8.65 M series/s with 4 queues and 3 contexts,
 # 9.5-9.7 with 8-16 queues and 6-8 contexts; C5's 8 search lanes: 4638 -> 5497 series/s; profiles/r03/j_hwq/{a,b}).
+# The C5 order search runs 16 search lanes, which need 16 + 2 queues (8 lanes on 8 queues: 10 654 series/s at
+# 262 144 x 1024; 16 lanes on 24 queues: 12 976; 16 lanes on 16 queues: no gain over 8, profiles/r03/q_lanes).
 # Set before anything initialises HIP (the GPU boxes export 4); a larger setting in the environment is kept.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or "4") < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+_C5 = any(a == "--config=c5" for a in sys.argv) or any(
+    a == "--config" and i + 1 < len(sys.argv) and sys.argv[i + 1] == "c5" for i, a in enumerate(sys.argv))
+_QUEUES = 24 if _C5 else 8
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or "4") < _QUEUES:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(_QUEUES)
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "spark-timeseries_amd"))
@@ -209,6 +214,7 @@ def main():
     ap.add_argument("--e2e", type=int, default=1, choices=[0, 1])
     ap.add_argument("--fit-kernel", type=int, default=-1, help="0: k_cg_fit (LDS slots), 2: rounds of streaming passes; -1: default")
     ap.add_argument("--device", type=int, default=None, help="GPU of every rank (default: LOCAL_RANK's)")
+    ap.add_argument("--search-lanes", type=int, default=0, help="c5: concurrent search lanes (0: 16)")
     ap.add_argument("--dry-run", action="store_true")
     args = ap.parse_args()
     if args.device is not None:
@@ -279,6 +285,8 @@ def main():
         eng.set_option("fit_kernel", args.fit_kernel)
     if args.grid_blocks:
         eng.set_option("grid_blocks", args.grid_blocks)
+    if args.config == "c5":
+        eng.set_option("search_lanes", args.search_lanes or 16)
 
     series = torch.empty((N, T), dtype=torch.float64, device=dev)
     eng.sample_device(series.data_ptr(), N, T, T, p, d, q, I, base, jitter, SEED, first)
@@ -487,7 +495,9 @@ def run_c5(args, eng, series, N, T, total_series, world, rank, dev, barrier, dis
                                    f"({'total over ' + str(world) + ' GPU(s)' if scaling == 'strong' else 'per GPU'};"
                                    f" BASELINE.json configs[4])",
                        "series_per_gpu": N, "series_total": total_series, "fits_per_series": 216,
-                       "fits_per_sec": total_series * 216 * args.steps / elapsed, "search_lanes": 8,
+                       "fits_per_sec": total_series * 216 * args.steps / elapsed,
+                       "search_lanes": eng.get_option("search_lanes"),
+                       "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                        "found_fraction": found, "selected_orders_top":
                            dict(sorted(sel.items(), key=lambda kv: -kv[1])[:6]),
                        "parallelism": f"series-sharded x{world}, no collective"},
