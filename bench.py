@@ -67,28 +67,20 @@ SEED = 20261015
 
 def build_sha():
     """sha256 of the HIP library this run loads: the key that ties carried PMC numbers to the measured build."""
-    import hashlib
-    h = hashlib.sha256()
-    try:
-        with open(os.environ.get("SPARKTS_ARIMA_LIB", LIB_PATH), "rb") as f:
-            for blk in iter(lambda: f.read(1 << 22), b""):
-                h.update(blk)
-    except OSError:
-        return None
-    return h.hexdigest()
+    from sparkts_amd.buildinfo import library_sha
+    return library_sha()
 
 
 def pmc_traffic(workload, sha):
-    """Carried PMC record of this workload AND this build (library sha256); None for any mismatch."""
+    """Carried PMC record of this workload AND this build: the library's sha256, else the sha256 of the build's
+    inputs (hipcc output is not byte-reproducible, sparkts_amd/buildinfo.py). (None, None) for any mismatch."""
+    from sparkts_amd.buildinfo import match_record, source_sha
     try:
         with open(PMC_TRAFFIC_FILE) as f:
             recs = json.load(f)
     except (OSError, ValueError):
-        return None
-    for m in recs if isinstance(recs, list) else [recs]:
-        if m.get("workload") == workload and sha is not None and m.get("build_sha") == sha:
-            return m
-    return None
+        return None, None
+    return match_record(recs if isinstance(recs, list) else [recs], workload, sha, source_sha())
 
 
 def physical_cores():
@@ -369,7 +361,7 @@ def main():
 
     if rank == 0:
         sha = build_sha()
-        pmc = pmc_traffic({"series": N, "T": T, "p": p, "d": d, "q": q, "I": int(I), "smear": args.smear}, sha)
+        pmc, pmc_key = pmc_traffic({"series": N, "T": T, "p": p, "d": d, "q": q, "I": int(I), "smear": args.smear}, sha)
         result = {
             "metric": "series fitted/sec, ARIMA(2,1,2) CSS-CGD, 1M x 1024 pts" if args.config == "c2"
             else f"series fitted/sec, {args.config}",
@@ -414,6 +406,7 @@ def main():
                          "traffic_source": pmc["source"] if pmc else
                          "no rocprofv3 PMC record of this workload for this build (library sha256 " + str(sha)[:16] + ")",
                          "build_sha": sha,
+                         "traffic_matched_on": pmc_key,
                          "hbm_GBps_pmc": (pmc["hbm_bytes_per_launch"] / (cg_ms * 1e-3) / 1e9) if pmc and cg_ms else None,
                          "hbm_frac_pmc": (pmc["hbm_bytes_per_launch"] / (cg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS)
                          if pmc and cg_ms else None,

@@ -112,12 +112,13 @@ int         arima_get_last_stats(const arima_handle *h, arima_fit_stats *out);
 /* Blocks until the device work of every call issued on the handle so far has finished. */
 int         arima_synchronize(arima_handle *h);
 /* Tuning knobs (not part of the reference contract): "smear" (Breeze reading at ARIMA.scala:526, default 1),
- * "fit_pipeline" (fit contexts in rotation for *_device fits, 1..4, default 1), "host_chunk" / "host_pipeline"
+ * "fit_pipeline" (fit contexts in rotation for *_device fits, 1..8, default 1), "host_chunk" / "host_pipeline"
  * (series per chunk and contexts of the chunked host path, default 262144 / 3), "express_blocks",
  * "grid_blocks", "search_lanes" (in-kernel scheduler and order-search concurrency), "fit_kernel" (0: k_cg_fit with
  * LDS-resident optimizer slots; 2: rounds of streaming passes, then k_cg_fit on the last series), "rounds_max",
  * "rounds_tail", "rounds_pass_waves" (fit_kernel 2), "hr_grid" (k_hr_init grid), "fit_slice_bytes"
- * (differenced workspace of one slice of a large device fit), "express_ring" (express hand-offs per launch). */
+ * (differenced workspace of one slice of a large device fit), "express_ring" (express hand-offs per launch),
+ * "row_pad" (doubles added to the stride of the differenced-row workspaces, whole 128-B lines, default 0). */
 int         arima_set_option(arima_handle *h, const char *name, int64_t value);
 /* Current value of a tuning knob (the names arima_set_option takes); ARIMA_E_INVALID_ARG for an unknown name. */
 int         arima_get_option(const arima_handle *h, const char *name, int64_t *value);

@@ -132,6 +132,7 @@ struct arima_handle {
     int express_blocks = -1;       // k_cg_fit express workgroups (-1: num_cus / 16)
     int express_ring = 0;          // express hand-offs per launch (0: the whole ring, sts::kExpressRingEntries)
     int hr_grid = 0;               // k_hr_init: 0 = a lane per series; > 0 = that many single-wave workgroups
+    int row_pad = 0;               // doubles (multiple of 16) added to the differenced rows' stride
     int fit_kernel = 0;            // 0: k_cg_fit (LDS slots, 1 wave/SIMD); 2: rounds of streaming passes + k_cg_fit
     int rounds_max = 96;           // rounds enqueued per fit (fit_kernel 2)
     int64_t rounds_tail = -1;      // a round with at most this many requests hands them to k_cg_fit (-1: half its slots)
@@ -186,6 +187,8 @@ int set_err(arima_handle *h, int code, const char *msg) {
     } while (0)
 
 inline int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+// Leading dimension of a differenced-row workspace: 128-B aligned rows of n doubles plus the handle's row_pad
+static int64_t row_stride(const arima_handle *h, int64_t n) { return round_up(std::max<int64_t>(n, 1), 16) + h->row_pad; }
 
 // uniform-per-call status fill (unsupported method, zero parameters, shape errors)
 __global__ void k_fill_status(int64_t N, int k, const int32_t *__restrict__ prior, int32_t code,
@@ -413,6 +416,10 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
         h->rounds_pass_waves = (int)std::min<int64_t>(32, std::max<int64_t>(1, value));
         return ARIMA_OK;
     }
+    if (!strcmp(name, "row_pad")) {                 // doubles, rounded up to whole 128-B lines
+        h->row_pad = (int)round_up(std::min<int64_t>(4096, std::max<int64_t>(0, value)), 16);
+        return ARIMA_OK;
+    }
     if (!strcmp(name, "hr_grid")) { h->hr_grid = (int)std::min<int64_t>(1 << 20, std::max<int64_t>(0, value)); return ARIMA_OK; }
     if (!strcmp(name, "express_ring")) {
         h->express_ring = (int)std::min<int64_t>(sts::kExpressRingEntries, std::max<int64_t>(0, value));
@@ -445,7 +452,7 @@ int arima_get_option(const arima_handle *hc, const char *name, int64_t *value) {
         {"smear", h->smear}, {"express_blocks", h->express_blocks}, {"grid_blocks", h->grid_blocks_override},
         {"search_lanes", h->search_lanes}, {"fit_pipeline", h->pipeline}, {"host_pipeline", h->host_pipeline},
         {"host_chunk", h->host_chunk}, {"fit_slice_bytes", h->fit_slice_bytes}, {"express_ring", h->express_ring},
-        {"fit_kernel", h->fit_kernel}, {"hr_grid", h->hr_grid}, {"rounds_max", h->rounds_max},
+        {"fit_kernel", h->fit_kernel}, {"hr_grid", h->hr_grid}, {"row_pad", h->row_pad}, {"rounds_max", h->rounds_max},
         {"rounds_tail", h->rounds_tail}, {"rounds_pass_waves", h->rounds_pass_waves},
         {"rounds_tail_express", h->rounds_tail_express}, {"rounds_tail_cus", h->rounds_tail_cus},
         {"rounds_tail_xcus", h->rounds_tail_xcus}};
@@ -628,7 +635,7 @@ static int fit_device_locked(arima_handle *h, FitCtx &c, int ci, int reserve, co
     HIPCHK(h, hipSetDevice(h->device));
     const int k = I + p + q;
     const int n = std::max(T - d, 0);
-    const int64_t ldn = round_up(std::max(n, 1), 16);
+    const int64_t ldn = row_stride(h, n);
     c.pending = PendingStats{};
     if (slot < 0) {
         h->stats = arima_fit_stats{};
@@ -743,7 +750,7 @@ int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_se
     std::lock_guard<std::mutex> lk(h->mu);
     const int P = h->pipeline;
     HIPCHK(h, hipSetDevice(h->device));
-    const int64_t ldn = round_up(std::max(T - d, 1), 16);
+    const int64_t ldn = row_stride(h, T - d);
     // Slice size: option fit_slice_bytes, or (0, the default) as large as the free HBM allows for P contexts. Every
     // slice ends with its own slowest series (the launch's critical path), so fewer, larger slices are faster (C4 at
     // 1M x 4096 in 262k-series slices: 2.9 s per fit alone, one slice: 1.2 s).
@@ -1014,7 +1021,7 @@ int arima_inverse_difference_batch(arima_handle *h, const double *series, int64_
 
 // upload N rows of length n into the padded (ld multiple of 16) workspace h->diff
 static int upload_padded(arima_handle *h, const double *src, int64_t N, int32_t n, int64_t *ld_out, hipStream_t s) {
-    const int64_t ld = round_up(std::max(n, 1), 16);
+    const int64_t ld = row_stride(h, n);
     RCCHK(h, h->diff.ensure((size_t)N * ld * sizeof(double)), "workspace");
     if (n > 0)
         HIPCHK(h, hipMemcpy2DAsync(h->diff.ptr, ld * sizeof(double), src, (size_t)n * sizeof(double),
@@ -1035,7 +1042,7 @@ int arima_css_loglik_batch(arima_handle *h, const double *series, int64_t N, int
     begin_call(h, s);
     const int k = I + p + q;
     const int n = std::max(T - d, 0);
-    const int64_t ldn = round_up(std::max(n, 1), 16);
+    const int64_t ldn = row_stride(h, n);
     RCCHK(h, h->h_series.ensure((size_t)N * std::max(T, 1) * sizeof(double)), "staging");
     RCCHK(h, h->diff.ensure((size_t)N * ldn * sizeof(double)), "workspace");
     RCCHK(h, h->h_coef.ensure((size_t)N * std::max(k, 1) * sizeof(double)), "staging");
@@ -1191,7 +1198,7 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
     // draining -- when they fit in HBM next to the lanes' workspaces; otherwise one shared copy, rewritten for each
     // d once every fit of the previous d has finished (max_d up to 16 would not fit).
     size_t diff_bytes = 0;
-    for (int d = 0; d <= max_d; ++d) diff_bytes += (size_t)N * round_up(std::max(T - d, 1), 16) * sizeof(double);
+    for (int d = 0; d <= max_d; ++d) diff_bytes += (size_t)N * row_stride(h, T - d) * sizeof(double);
     const size_t lane_bytes = (size_t)N * (11 * 8 * 2 + 8 + 4 * 4 + 1 + 8 + 16 + 88) + sts::kExpressRingBytes +
                               sts::kExpressReadyBytes;
     size_t free_b = 0, total_b = 0;
@@ -1232,14 +1239,14 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
     }
     if (per_d) {
         for (int d = 0; d <= max_d; ++d)
-            RCCHK(h, h->os_diff[d].ensure((size_t)N * round_up(std::max(T - d, 1), 16) * sizeof(double)), "workspace");
+            RCCHK(h, h->os_diff[d].ensure((size_t)N * row_stride(h, T - d) * sizeof(double)), "workspace");
     } else {
-        RCCHK(h, h->os_diff[0].ensure((size_t)N * round_up(std::max(T, 1), 16) * sizeof(double)), "workspace");
+        RCCHK(h, h->os_diff[0].ensure((size_t)N * row_stride(h, T) * sizeof(double)), "workspace");
     }
     HIPCHK(h, hipEventRecord(h->ev[0], s));
     auto diff_into = [&](int d, DevBuf &buf) -> int {
         const int n = std::max(T - d, 0);
-        const int64_t ldn = round_up(std::max(n, 1), 16);
+        const int64_t ldn = row_stride(h, n);
         if (!h->ev_diff[d]) HIPCHK(h, hipEventCreateWithFlags(&h->ev_diff[d], hipEventDisableTiming));
         RCCHK(h, sts::launch_difference(d_series, ld, buf.as<double>(), ldn, N, T, d, 1, s), "difference");
         HIPCHK(h, hipEventRecord(h->ev_diff[d], s));
@@ -1296,7 +1303,7 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
                 if (!per_d && gp.d != dd) continue;
                 const int d = gp.d, p = gp.p, q = gp.q, I = gp.I;
                 const int n = std::max(T - d, 0);
-                const int64_t ldn = round_up(std::max(n, 1), 16);
+                const int64_t ldn = row_stride(h, n);
                 DevBuf &dbuf = per_d ? h->os_diff[d] : h->os_diff[0];
                 HIPCHK(h, hipStreamWaitEvent(ln.stream, h->ev_diff[d], 0));
                 // ARIMA(0,d,0) without intercept has no parameters: the reference throws (NoDataException);

@@ -592,6 +592,37 @@ def test_express_ring_cap_is_transparent(engine):
         assert _same(x, y)
 
 
+def test_row_pad_is_transparent(engine):
+    # option row_pad widens the differenced rows' stride (whole 128-B lines) so that the rows of concurrently
+    # streamed series stop sharing the low address bits; results must not move by a bit, on the fit path and on the
+    # order search (which keeps one differenced copy per d)
+    import torch
+    N, T = 8192, 1024
+    s = _device_sample(engine, N, T, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 7)
+    host = s.cpu().numpy()[:512]
+    outs = {}
+    for pad in (0, 40):
+        engine.set_option("row_pad", pad)
+        try:
+            assert engine.get_option("row_pad") == (48 if pad else 0)
+            r = [torch.empty((N, 5), dtype=torch.float64, device=s.device),
+                 torch.empty(N, dtype=torch.float64, device=s.device)] + \
+                [torch.empty(N, dtype=torch.int32, device=s.device) for _ in range(3)] + \
+                [torch.empty(N, dtype=torch.uint8, device=s.device)]
+            engine.fit_batch_device(s.data_ptr(), N, T, T, 2, 1, 2, True, *[t.data_ptr() for t in r])
+            st = engine.stats()
+            srch = engine.order_search(host, 2, 1, 2, 2)
+        finally:
+            engine.set_option("row_pad", 0)
+        outs[pad] = ([t.cpu().numpy() for t in r], st, srch)
+    (a, sa, qa), (b, sb, qb) = outs[0], outs[40]
+    assert sb["series_done"] == N and sb["fault"] == 0 and sa["n_eval"] == sb["n_eval"]
+    for x, y in zip(a, b):
+        assert _same(x, y)
+    for x, y in zip(qa, qb):
+        assert _same(np.asarray(x), np.asarray(y))
+
+
 ROUNDS_CONFIGS = {
     # every series through the rounds (hand-off only in the last round, past every fit's end)
     "all_rounds": dict(rounds_max=400, rounds_tail=0),

@@ -92,14 +92,14 @@ def main():
     txt = "\n".join(lines)
     fit = next((v for k, v in cs.items() if k.startswith("k_cg_fit")), {})
     if traffic_path and "FETCH_SIZE" in fit and "WRITE_SIZE" in fit:
-        import hashlib
         import json
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                        "spark-timeseries_amd"))
+        from sparkts_amd.buildinfo import library_sha, source_sha
         rd = sum(fit["FETCH_SIZE"]) / len(fit["FETCH_SIZE"]) * 1024 * 2
         wr = sum(fit["WRITE_SIZE"]) / len(fit["WRITE_SIZE"]) * 1024
-        lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "spark-timeseries_amd",
-                           "libsparkts_arima.so")
-        sha = hashlib.sha256(open(lib, "rb").read()).hexdigest()
-        out = {"workload": workload, "build_sha": sha,
+        sha = library_sha()
+        out = {"workload": workload, "build_sha": sha, "source_sha": source_sha(),
                "kernel": "k_cg_fit", "hbm_bytes_per_launch": rd + wr, "read_bytes": rd, "write_bytes": wr,
                "source": source or root}
 
