@@ -9,7 +9,7 @@ namespace sts {
 int launch_difference(const double *in, int64_t ld_in, double *out, int64_t ld_out, int64_t N, int T, int d,
                       int drop, hipStream_t s);
 int launch_search_init(double *best_aic, int32_t *order, double *coef, int64_t N, hipStream_t s);
-constexpr int kSearchMaxLanes = 16;
+constexpr int kSearchMaxLanes = 32;
 struct SearchBests {               // the order search's per-lane best candidates (by value into k_search_merge)
     const double *aic[kSearchMaxLanes];
     const int32_t *order[kSearchMaxLanes];

@@ -512,6 +512,24 @@ def test_order_search_T1024_matches_oracle(engine):
     assert _same(aic, ea)
 
 
+def test_order_search_lane_count_is_transparent(engine):
+    # every lane keeps its own best per series and candidates compare by (approxAIC, grid position), so the outcome
+    # cannot depend on how many lanes run the grid or in which order their fits finish: 1, 8 (default), 32 lanes
+    s = _device_sample(engine, 4096, 512, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 99).cpu().numpy()
+    res = {}
+    for lanes in (1, 8, 32):
+        engine.set_option("search_lanes", lanes)
+        try:
+            assert engine.get_option("search_lanes") == lanes
+            res[lanes] = engine.order_search(s, 3, 2, 3, 2)
+        finally:
+            engine.set_option("search_lanes", 8)
+    for lanes in (1, 32):
+        for x, y in zip(res[8], res[lanes]):
+            assert _same(np.asarray(x), np.asarray(y)), lanes
+    assert np.all(res[8][0][:, 0] >= 0)
+
+
 def test_wire_format_partition_fit_matches_oracle(engine):
     # records in the JVM <-> Python wire format (PythonConnector.scala:59-88) through fit_arima_records: the
     # coefficients that come back, decoded, equal the oracle's (NaN for failed fits); two series lengths in one
