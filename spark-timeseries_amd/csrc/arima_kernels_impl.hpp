@@ -216,6 +216,12 @@ constexpr bool kFRide = STS_F_RIDE != 0;     // objective requests fill the idle
 #define STS_OLD_EVALS 128
 #endif
 constexpr int kOldEvals = STS_OLD_EVALS;     // evaluations after which a series is served with priority
+#ifndef STS_ADV_REGS
+#define STS_ADV_REGS 0                       // bulk optimizer steps on a register copy of the LDS slot (A/B: DESIGN 7.2)
+#endif
+#ifndef STS_ADV_REGS_X
+#define STS_ADV_REGS_X 0                     // ... and the express waves' (measured slower: profiles/r03/v_adv)
+#endif
 
 constexpr int kFitLdsBudget = 160 * 1024 - 1024;
 // slots per wave: as many as the LDS holds, at most 2 per lane, a multiple of 8 (at least 64 unless more than
@@ -507,21 +513,31 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
         if (req == REQ_G && gl < K) xch[gl] = gj;
         if (req == REQ_G && glead) xch[K] = css_to_loglik(cssv, n);
         wave_sync_lds();
-        if (glead && req == REQ_F) {
-            for (int h = 1; h <= nsp && h <= NS; ++h) ES.s.spec_store(h - 1, xch[h]);
-            double g0[K];
+        if (glead && req != REQ_NONE) {
+#if STS_ADV_REGS_X
+            CGLane<K, NS, spec_nc<K>()> L = ES.s;           // the long series' critical path: state in registers
+#else
+            CGLane<K, NS, spec_nc<K>()> &L = ES.s;
+#endif
+            if (req == REQ_F) {
+                for (int h = 1; h <= nsp && h <= NS; ++h) L.spec_store(h - 1, xch[h]);
+                double g0[K];
 #pragma unroll
-            for (int j = 0; j < K; ++j) g0[j] = 0.0;
-            ES.s.req = REQ_NONE;
-            ES.s.advance(xch[0], g0);
-            pf++;
-        } else if (glead && req == REQ_G) {
-            double g[K];
+                for (int j = 0; j < K; ++j) g0[j] = 0.0;
+                L.req = REQ_NONE;
+                L.advance(xch[0], g0);
+                pf++;
+            } else {
+                double g[K];
 #pragma unroll
-            for (int j = 0; j < K; ++j) g[j] = xch[j];
-            ES.s.req = REQ_NONE;
-            ES.s.advance(xch[K], g);
-            pg++;
+                for (int j = 0; j < K; ++j) g[j] = xch[j];
+                L.req = REQ_NONE;
+                L.advance(xch[K], g);
+                pg++;
+            }
+#if STS_ADV_REGS_X
+            ES.s = L;
+#endif
         }
         wave_sync_lds();
         // ---- finished series: write the result, take a new ticket ----
@@ -727,7 +743,16 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
 #pragma unroll
             for (int jj = 0; jj < NJ; ++jj) {
                 const int j = (jj + (int)round_no) % NJ;
-                unsigned long long m = ((doG && tier < 2) ? mG[j] : mF[j]) & ((tier & 1) == 0 ? mO[j] : ~mO[j]);
+                // select the slot group's masks without a dynamically indexed register array (that would live in
+                // scratch memory: 4 scratch loads per pass selection)
+                unsigned long long wG = mG[0], wF = mF[0], wO = mO[0];
+#pragma unroll
+                for (int i = 1; i < NJ; ++i) {
+                    wG = (j == i) ? mG[i] : wG;
+                    wF = (j == i) ? mF[i] : wF;
+                    wO = (j == i) ? mO[i] : wO;
+                }
+                unsigned long long m = ((doG && tier < 2) ? wG : wF) & ((tier & 1) == 0 ? wO : ~wO);
                 m = (m >> rot) | (rot ? (m << (64 - rot)) : 0ull);          // rotate: lane rot ranks first
                 const int lr = (lane - rot) & 63;
                 if ((m >> lr) & 1ull) {
@@ -818,22 +843,32 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
 #endif
         bool need = false;
         if (served) {
-            S.s.req = REQ_NONE;
-            S.s.advance(resp_f, g);
-            if (S.s.done()) {
+#if STS_ADV_REGS
+            // the state machine runs on a register copy of the slot: inside advance() every field access would
+            // otherwise be an LDS access whose latency one wave per SIMD cannot hide
+            CGLane<K, NS, spec_nc<K>()> L = S.s;
+#else
+            CGLane<K, NS, spec_nc<K>()> &L = S.s;
+#endif
+            L.req = REQ_NONE;
+            L.advance(resp_f, g);
+            if (L.done()) {
                 double pt[K];
 #pragma unroll
-                for (int j = 0; j < K; ++j) pt[j] = S.s.point[j];
-                write_fit<K>(S.sid, S.s.status, pt, S.s.prev_obj, S.s.n_eval, S.s.n_grad,
-                             S.s.status == ARIMA_ST_OK ? model_flags<P, Q, I>(pt) : (uint8_t)0, coef_out, ll_out,
+                for (int j = 0; j < K; ++j) pt[j] = L.point[j];
+                write_fit<K>(S.sid, L.status, pt, L.prev_obj, L.n_eval, L.n_grad,
+                             L.status == ARIMA_ST_OK ? model_flags<P, Q, I>(pt) : (uint8_t)0, coef_out, ll_out,
                              status_out, n_eval_out, n_grad_out, flags_out);
                 timing_stamp<K>(S, coef_out);
-                evals += S.s.n_eval;
-                grads += S.s.n_grad;
-                hits += S.s.spec_hits;
+                evals += L.n_eval;
+                grads += L.n_grad;
+                hits += L.spec_hits;
                 done++;
                 need = true;
             }
+#if STS_ADV_REGS
+            S.s = L;
+#endif
         }
         refill(my, need);
         if (has_express) {
