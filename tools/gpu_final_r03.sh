@@ -4,7 +4,7 @@
 # Every GPU step has its own time limit; the chain stops at the first failure. Run ON the GPU box from the repo root.
 cd /tmp && export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-OUT=gpurun_out/r03/final2
+OUT=gpurun_out/${FINAL_OUT:-r03/final2}
 mkdir -p $OUT
 timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 &&
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 &&
