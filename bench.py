@@ -80,7 +80,10 @@ def pmc_traffic(workload, sha):
             recs = json.load(f)
     except (OSError, ValueError):
         return None, None
-    return match_record(recs if isinstance(recs, list) else [recs], workload, sha, source_sha())
+    # the source fallback only for the default library: a dev library (SPARKTS_ARIMA_LIB) is built from the same
+    # sources with extra -D flags that the source sha cannot see
+    src = None if os.environ.get("SPARKTS_ARIMA_LIB") else source_sha()
+    return match_record(recs if isinstance(recs, list) else [recs], workload, sha, src)
 
 
 def physical_cores():
@@ -141,13 +144,17 @@ def cpu_baseline(series_host, p, d, q, I, smear, target_s):
     cores = int(omp_env or "0") or affinity
     cores = max(1, min(cores, affinity, 64))
 
+    first = {}
+
     def timed(threads, sample, budget):
         os.environ["OMP_NUM_THREADS"] = str(threads)
         O.set_threads(threads)
         done, rounds, conv = 0, 0, 0
         t0 = time.perf_counter()
         while True:
-            st, _, _, _ = O.fit_batch(sample, p, d, q, I, smear=smear)
+            st, coef, ll, cnt = O.fit_batch(sample, p, d, q, I, smear=smear)
+            if not first:                  # the oracle's results, for the parity check of the timed step
+                first.update(status=st, coef=coef, ll=ll, n_eval=cnt[:, 0], n_grad=cnt[:, 1])
             done += len(sample)
             rounds += 1
             conv = int((st == 0).sum())
@@ -157,12 +164,13 @@ def cpu_baseline(series_host, p, d, q, I, smear, target_s):
 
     O.lib()
     rate, rounds, conv = timed(cores, series_host, target_s)
+    oracle_rows = dict(first)
     one = series_host[: max(1, len(series_host) // 16)]
     rate1, rounds1, _ = timed(1, one, max(2.0, target_s / 3))
     os.environ["OMP_NUM_THREADS"] = str(cores)
     O.set_threads(cores)
     phys = physical_cores()
-    return {"value": rate, "unit": "series fitted/sec", "cores": cores, "kind": "port",
+    return oracle_rows, {"value": rate, "unit": "series fitted/sec", "cores": cores, "kind": "port",
             "value_1core": rate1, "host_physical_cores": phys, "host_cpus": os.cpu_count(), "affinity_cpus": affinity,
             "projected_all_physical_cores": rate1 * phys if phys else None,
             "sample": f"{len(series_host)} synthetic series of the benchmark workload (first rows of rank 0's shard) "
@@ -172,6 +180,41 @@ def cpu_baseline(series_host, p, d, q, I, smear, target_s):
                       f"value_1core: the first {len(one)} of them {rounds1}x on one thread; "
                       f"projected_all_physical_cores = value_1core x physical cores (linear, not measured); "
                       f"not the spark-ts JVM"}
+
+
+def same_bits(a, b):
+    """Per-row bitwise equality of two device tensors of the same shape (rows = series)."""
+    import torch
+    if a.dtype == torch.float64:
+        a, b = a.view(torch.int64), b.view(torch.int64)
+    eq = a == b
+    return eq.reshape(eq.shape[0], -1).all(dim=1) if eq.dim() > 1 else eq
+
+
+def outputs_match(x, y):
+    """Series whose every output (coef, LL, status, n_eval, n_grad, flags) is bit-identical in x and y."""
+    ok = None
+    for k in ("coef", "ll", "status", "n_eval", "n_grad", "flags"):
+        e = same_bits(x[k], y[k])
+        ok = e if ok is None else ok & e
+    return ok
+
+
+def oracle_row_parity(res, exp):
+    """Rows of the timed step bit-identical to the oracle (status, n_eval, n_grad exact; coef, LL and flags bit for
+    bit where the fit returned normally, NaN coefficients where it failed): the count of matching rows."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    st = exp["status"]
+    ok = (res["status"] == st) & (res["n_eval"] == exp["n_eval"]) & (res["n_grad"] == exp["n_grad"])
+    good = st == 0
+    cb = res["coef"].view(np.int64) == exp["coef"].view(np.int64)
+    lb = res["ll"].view(np.int64) == exp["ll"].view(np.int64)
+    p, q, I = exp["pqi"]
+    fl = np.array([O.model_flags(exp["coef"][i], p, q, I) if good[i] else 0 for i in range(len(st))], dtype=np.uint8)
+    ok &= np.where(good, cb.all(axis=1) & lb & (res["flags"] == fl), np.isnan(res["coef"]).all(axis=1))
+    return int(ok.sum())
 
 
 def end_to_end(eng, series, p, d, q, I):
@@ -341,6 +384,8 @@ def main():
         return U * S * ff + G * S * fg, U, G
 
     flops_step, U, G = cg_flops(s0)
+    # the last timed step's outputs, kept for the parity checks below (the isolated step may reuse its buffers)
+    last = {k: v.clone() for k, v in outs[(calls[0] - 1) % len(outs)].items()}
     # the dominant kernel's own launch duration: one more step alone on the GPU (fit_pipeline 1), HIP events
     eng.set_option("fit_pipeline", 1)
     step()
@@ -349,6 +394,13 @@ def main():
     if s1["series_done"] != N:
         raise SystemExit(f"bench.py: the isolated step wrote {s1['series_done']} of {N} results")
     eng.set_option("fit_pipeline", args.pipeline)
+    # parity of the configuration that was timed: the last pipelined step against the isolated step,
+    # every series, bit for bit (max over ranks of the mismatching series)
+    iso = outs[(calls[0] - 1) % len(outs)]
+    iso_mismatch = int(max_over_ranks(float(N - int(outputs_match(last, iso).sum().item())),
+                                      dist if world > 1 else None))
+    if iso_mismatch:
+        log(f"[rank {rank}] PARITY: {iso_mismatch} series of the timed step differ from the isolated step")
     flops_iso, _, _ = cg_flops(s1)
     cg_ms = s1["ms_cg_fit"]
     achieved_tf = flops_iso / (cg_ms * 1e-3) / 1e12 if cg_ms > 0 else 0.0
@@ -361,7 +413,11 @@ def main():
 
     if rank == 0:
         sha = build_sha()
-        pmc, pmc_key = pmc_traffic({"series": N, "T": T, "p": p, "d": d, "q": q, "I": int(I), "smear": args.smear}, sha)
+        # the record key names the fit kernel and any non-default engine options too: a record of another variant
+        # never stands for this run's kernel
+        pmc, pmc_key = pmc_traffic({"series": N, "T": T, "p": p, "d": d, "q": q, "I": int(I), "smear": args.smear,
+                                    "fit_kernel": eng_fit_kernel(eng),
+                                    "options": os.environ.get("SPARKTS_OPTIONS", "")}, sha)
         result = {
             "metric": "series fitted/sec, ARIMA(2,1,2) CSS-CGD, 1M x 1024 pts" if args.config == "c2"
             else f"series fitted/sec, {args.config}",
@@ -424,9 +480,22 @@ def main():
         }
         if world == 1 and args.e2e:
             result["end_to_end_host"] = end_to_end(eng, series, p, d, q, I)
+        parity = {"configuration": f"the last timed step: fit_pipeline {args.pipeline} on GPU_MAX_HW_QUEUES="
+                                   f"{os.environ.get('GPU_MAX_HW_QUEUES')}",
+                  "vs_isolated": iso_mismatch == 0, "isolated_mismatch_series": iso_mismatch,
+                  "isolated_compared_series": total_series, "oracle_rows": 0, "bit_identical": None}
         if world == 1 and args.cpu_seconds > 0:
             host = series[: 4096].cpu().numpy()
-            result["cpu_baseline"] = cpu_baseline(host, p, d, q, I, args.smear, args.cpu_seconds)
+            exp, result["cpu_baseline"] = cpu_baseline(host, p, d, q, I, args.smear, args.cpu_seconds)
+            rows = len(host)
+            res = {k: v[:rows].cpu().numpy() for k, v in last.items()}
+            exp["pqi"] = (p, q, int(I))
+            parity["oracle_rows"] = rows
+            parity["bit_identical"] = oracle_row_parity(res, exp)
+            parity["oracle_source"] = "oracle/arima_oracle.c on rows 0..%d (the cpu_baseline sample)" % (rows - 1)
+            if parity["bit_identical"] != rows:
+                log(f"PARITY: {rows - parity['bit_identical']} of {rows} oracle rows differ from the timed step")
+        result["parity"] = parity
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()

@@ -125,19 +125,21 @@ static void differences_at_lag(const double *ts, double *dest, int n, int lag, i
 void orc_differences_of_order_d(const double *ts, int T, int d, double *out) {
     double *diffed = (double *)malloc(sizeof(double) * (size_t)(T > 0 ? T : 1));
     double *orig = (double *)malloc(sizeof(double) * (size_t)(T > 0 ? T : 1));
-    memcpy(diffed, ts, sizeof(double) * (size_t)T);
-    memcpy(orig, ts, sizeof(double) * (size_t)T);
+    if (T > 0) {                                  /* (an empty series may come with a null pointer) */
+        memcpy(diffed, ts, sizeof(double) * (size_t)T);
+        memcpy(orig, ts, sizeof(double) * (size_t)T);
+    }
     for (int i = 1; i <= d; i++) {
         double *swap = orig; orig = diffed; diffed = swap;
         differences_at_lag(orig, diffed, T, 1, i);
     }
-    memcpy(out, diffed, sizeof(double) * (size_t)T);
+    if (T > 0) memcpy(out, diffed, sizeof(double) * (size_t)T);
     free(diffed); free(orig);
 }
 
 /* inverseDifferencesOfOrderD  UnivariateTimeSeries.scala:489-495 (+ inverseDifferencesAtLag :426-447, in place) */
 void orc_inverse_differences_of_order_d(const double *in, int L, int d, double *out) {
-    memcpy(out, in, sizeof(double) * (size_t)L);
+    if (L > 0) memcpy(out, in, sizeof(double) * (size_t)L);
     for (int i = d; i >= 1; i--)
         for (int j = 0; j < L; j++) out[j] = (j < i) ? out[j] : out[j] + out[j - 1];
 }

@@ -281,7 +281,8 @@ def order_search(series, max_p=5, max_d=2, max_q=5, intercept_mode=2, method=0, 
                         if st[i] != 0 or model_flags(coef[i], p, q, I) != 3:
                             continue
                         aic = -2.0 * ll[i] + float(2 * k)
-                        if aic < aic_best[i]:
+                        # `_ < curBestAIC`, curBestAIC starting at Double.MaxValue (ARIMA.scala:323, :344)
+                        if aic < aic_best[i] and aic < 1.7976931348623157e308:
                             aic_best[i] = aic
                             order[i] = (p, d, q, I)
                             coef_best[i] = 0.0

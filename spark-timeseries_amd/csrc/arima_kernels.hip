@@ -361,9 +361,14 @@ __global__ __launch_bounds__(256) void k_search_select(const double *__restrict_
         return;
     const int k = I + p + q;
     const double aic = -2.0 * cand_ll[i] + (double)(2 * k);
-    // the first minimum in (d, p, q, intercept) order wins (minBy), whatever order the candidates arrive in
+    // autoFit keeps `_ < curBestAIC` with curBestAIC = Double.MaxValue at the start (ARIMA.scala:323, :344): a
+    // +inf or NaN approxAIC never qualifies, not even against the empty best
+    if (!(aic < 1.7976931348623157e308)) return;
+    // the first minimum in (d, p, q, intercept) order wins (minBy), whatever order the candidates arrive in; the
+    // grid-position tie-break applies only against a real candidate
     const double b = best_aic[i];
-    if (!(aic < b) && !(aic == b && search_key(p, d, q, I) < search_key(order + i * 4))) return;
+    const bool have = order[i * 4] >= 0;
+    if (have && !(aic < b) && !(aic == b && search_key(p, d, q, I) < search_key(order + i * 4))) return;
     best_aic[i] = aic;
     order[i * 4 + 0] = p;
     order[i * 4 + 1] = d;
@@ -385,6 +390,7 @@ __global__ __launch_bounds__(256) void k_search_merge(const SearchBests b, int l
         const int32_t *o = b.order[l] + i * 4;
         if (o[0] < 0) continue;
         const double a = b.aic[l][i];
+        if (!(a < 1.7976931348623157e308)) continue;    // never stored by k_search_select; kept for symmetry
         const int key = search_key(o);
         if (w < 0 || a < wa || (a == wa && key < wk)) {
             w = l;

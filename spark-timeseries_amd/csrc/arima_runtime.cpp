@@ -108,6 +108,7 @@ struct FitCtx {
     unsigned long long *ctl_host = nullptr;   // pinned
     PendingStats pending;
     bool fit_ctl = false;                     // ctl_host holds (or will hold, in stream order) the kernel counters
+    bool rounds_last = false;                 // the context's last fit ran the rounds fit (fit_kernel 2)
     // host path (arima_fit_batch): device copies of one chunk and pinned staging of its input and outputs
     DevBuf d_series, d_coef, d_ll, d_status, d_neval, d_ngrad, d_flags, d_uinit;
     void *pin = nullptr;
@@ -150,7 +151,8 @@ struct arima_handle {
     SliceSlot slot[kSliceSlots];
     unsigned long long *slot_ctl = nullptr;     // pinned, kCtlWords per slot
     unsigned slot_seq = 0;                      // slots taken so far
-    unsigned slice_first = 0, slice_n = 0;      // slots of the last sliced fit call (stats_ctx == -2)
+    unsigned slice_first = 0, slice_n = 0;      // slots of the last sliced fit call still pending (stats_ctx == -2)
+    arima_fit_stats slice_acc{};                // ... and the stats of its slices whose slots were already reused
     DevBuf dev_fault;                           // sticky device record of the first fit-kernel fault (6 words)
     unsigned fit_seq = 0;          // fit calls so far (selects the context)
     int stats_ctx = -1;            // context of the last fit (arima_get_last_stats), -1: none
@@ -205,6 +207,16 @@ __global__ void k_fill_status(int64_t N, int k, const int32_t *__restrict__ prio
     if (n_eval_out) n_eval_out[i] = 0;
     if (n_grad_out) n_grad_out[i] = 0;
     if (flags_out) flags_out[i] = 0;
+}
+
+// Take (read and clear) the sticky fault record rec[0..5] into rec[8..13] with atomic exchanges: a fault that a
+// concurrent k_fault_merge records after the exchange of rec[0] stays for the next take instead of being cleared
+// unseen (a plain read followed by a memset could lose it).
+__global__ void k_fault_take(unsigned long long *__restrict__ rec) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long code = atomicExch(&rec[0], 0ull);
+    rec[8] = code;
+    for (int i = 1; i < 6; ++i) rec[8 + i] = code ? atomicExch(&rec[i], 0ull) : 0ull;
 }
 
 // the first watchdog fault of a fit kernel (its ctl[26..31]) into the handle's sticky device record
@@ -273,8 +285,8 @@ int arima_create(int device, arima_handle **out) {
     if (rc == ARIMA_OK &&
         hipHostMalloc((void **)&h->slot_ctl, (size_t)kSliceSlots * kCtlWords * sizeof(unsigned long long), 0) != hipSuccess)
         rc = ARIMA_E_OOM;
-    if (rc == ARIMA_OK && h->dev_fault.ensure(8 * sizeof(unsigned long long)) != ARIMA_OK) rc = ARIMA_E_OOM;
-    if (rc == ARIMA_OK && hipMemset(h->dev_fault.ptr, 0, 8 * sizeof(unsigned long long)) != hipSuccess) rc = ARIMA_E_DEVICE;
+    if (rc == ARIMA_OK && h->dev_fault.ensure(16 * sizeof(unsigned long long)) != ARIMA_OK) rc = ARIMA_E_OOM;
+    if (rc == ARIMA_OK && hipMemset(h->dev_fault.ptr, 0, 16 * sizeof(unsigned long long)) != hipSuccess) rc = ARIMA_E_DEVICE;
     if (rc != ARIMA_OK) {
         arima_destroy(h);
         return rc;
@@ -338,7 +350,7 @@ int arima_get_last_stats(const arima_handle *hc, arima_fit_stats *out) {
         finish_stats(h, c);
     } else if (h->stats_ctx == -2 && h->slice_n > 0) {   // a sliced fit: the sum over its slices
         hipSetDevice(h->device);
-        arima_fit_stats acc{};
+        arima_fit_stats acc = h->slice_acc;
         for (unsigned j = 0; j < h->slice_n; ++j) {
             const unsigned sl = (h->slice_first + j) % kSliceSlots;
             SliceSlot &ss = h->slot[sl];
@@ -347,6 +359,7 @@ int arima_get_last_stats(const arima_handle *hc, arima_fit_stats *out) {
         }
         h->stats = acc;
         h->slice_n = 0;
+        h->slice_acc = arima_fit_stats{};
     }
     *out = h->stats;
     return ARIMA_OK;
@@ -373,7 +386,7 @@ int arima_rounds_trace(arima_handle *h, unsigned *out, int max_words) {
     if (h->stats_ctx < 0) return 0;
     FitCtx &c = h->fctx[h->stats_ctx];
     if (c.has_done) HIPCHK(h, hipEventSynchronize(c.ev_done));
-    if (!c.ws.rc.ptr) return 0;
+    if (!c.ws.rc.ptr || !c.rounds_last) return 0;     // no rounds words of the context's last fit
     const int words = (int)std::min<size_t>((size_t)max_words, c.ws.rc.bytes / sizeof(unsigned));
     HIPCHK(h, hipMemcpy(out, c.ws.rc.ptr, (size_t)words * sizeof(unsigned), hipMemcpyDeviceToHost));
     return words;
@@ -637,6 +650,7 @@ static int fit_device_locked(arima_handle *h, FitCtx &c, int ci, int reserve, co
     const int n = std::max(T - d, 0);
     const int64_t ldn = row_stride(h, n);
     c.pending = PendingStats{};
+    c.rounds_last = false;
     if (slot < 0) {
         h->stats = arima_fit_stats{};
         h->stats_ctx = ci;
@@ -668,6 +682,7 @@ static int fit_device_locked(arima_handle *h, FitCtx &c, int ci, int reserve, co
     ps.ar_only = p > 0 && q == 0;
     ps.user_init = d_user_init != nullptr;
     ps.cg = !ps.ar_only && method == ARIMA_METHOD_CSS_CGD && k > 0;
+    c.rounds_last = ps.cg && h->fit_kernel == 2;
     ps.grid = grid;
     ps.express = xblocks;
     ps.valid = true;
@@ -783,6 +798,7 @@ int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_se
     h->stats_ctx = -2;
     h->slice_first = h->slot_seq % kSliceSlots;
     h->slice_n = 0;
+    h->slice_acc = arima_fit_stats{};
     for (int64_t j = 0; j < nslices; ++j) {
         const int sl = (int)(h->slot_seq++ % kSliceSlots);
         SliceSlot &ss = h->slot[sl];
@@ -791,6 +807,13 @@ int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_se
             ss.used = true;
         } else if (hipEventQuery(ss.ev[4]) != hipSuccess) {
             HIPCHK(h, hipEventSynchronize(ss.ev[4]));       // its previous slice's counter copy must have landed
+        }
+        if (h->slice_n == (unsigned)kSliceSlots) {
+            // more slices than slots: the oldest pending slice of THIS call is the one in slot sl; fold its stats
+            // into the call's running total before the slot is overwritten
+            acc_stats(h->slice_acc, compute_stats(ss.ps, h->slot_ctl + (size_t)sl * kCtlWords, ss.ev));
+            h->slice_first = (h->slice_first + 1) % kSliceSlots;
+            h->slice_n--;
         }
         ss.ps = PendingStats{};
         const int64_t f = j * slice, ns = std::min(slice, n_series - f);
@@ -1351,9 +1374,12 @@ static void join_lanes(arima_handle *h, hipStream_t s) {
 // pass as a candidate, and the call reports ARIMA_E_DEVICE).
 static int take_fault(arima_handle *h) {
     unsigned long long f[6] = {};
-    HIPCHK(h, hipMemcpy(f, h->dev_fault.ptr, sizeof f, hipMemcpyDeviceToHost));
+    unsigned long long *rec = h->dev_fault.as<unsigned long long>();
+    hipLaunchKernelGGL(k_fault_take, dim3(1), dim3(64), 0, h->stream, rec);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipMemcpyAsync(f, rec + 8, sizeof f, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
     if (f[0] == 0) return ARIMA_OK;
-    HIPCHK(h, hipMemset(h->dev_fault.ptr, 0, 8 * sizeof(unsigned long long)));
     char msg[160];
     snprintf(msg, sizeof msg, "fit kernel watchdog fault %llu (info %llu %llu %llu %llu %llu)", f[0], f[1], f[2],
              f[3], f[4], f[5]);

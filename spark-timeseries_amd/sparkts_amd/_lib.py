@@ -158,7 +158,7 @@ class Engine:
             raise EngineError(f"arima_create(device={device}) failed with {rc}: no usable HIP device")
         self.h = h
         self.device = device
-        # engine-wide knobs from the environment (A/B runs of the test suite and the bench): SPARKTS_FIT_KERNEL=0|1
+        # engine-wide knobs from the environment (A/B runs of the test suite and the bench): SPARKTS_FIT_KERNEL=0|2
         if os.environ.get("SPARKTS_FIT_KERNEL", "") != "":
             self.set_option("fit_kernel", int(os.environ["SPARKTS_FIT_KERNEL"]))
         # any option: SPARKTS_OPTIONS="hr_grid=1024,fit_pipeline=2"

@@ -550,13 +550,15 @@ def test_wire_format_partition_fit_matches_oracle(engine):
         assert _same(c, exp[k]), k
 
 
-@pytest.mark.parametrize("pipeline", [1, 3])
-def test_sliced_device_fit_matches_unsliced(engine, pipeline):
+@pytest.mark.parametrize("pipeline,N", [(1, 5000), (3, 5000), (3, 70000)])
+def test_sliced_device_fit_matches_unsliced(engine, pipeline, N):
     # arima_fit_batch_device over more series than one slice (option fit_slice_bytes: 1024 series of T = 1024 here)
     # runs slice by slice over the fit contexts -- the path that bounds C3's 8M-series workspaces on one GPU. Results
-    # must equal the one-slice fit bit for bit, and the stats must sum over every slice.
+    # must equal the one-slice fit bit for bit, and the stats must sum over every slice. N = 70000 is 69 slices: more
+    # than the 64 slice slots, so slots are reused within one call and their stats must still be counted once each
+    # (ADVICE r3).
     import torch
-    N, T = 5000, 1024
+    T = 1024
     s = _device_sample(engine, N, T, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 4242)
 
     def run():
@@ -579,6 +581,7 @@ def test_sliced_device_fit_matches_unsliced(engine, pipeline):
         assert _same(x, y)
     assert st["n_series"] == N and st["n_eval"] == int(whole[3].sum()) and st["n_grad"] == int(whole[4].sum()), st
     assert st["n_eval"] == st_whole["n_eval"] and st["ms_cg_fit"] > 0
+    assert st["series_done"] == N, st
 
 
 def test_express_ring_cap_is_transparent(engine):

@@ -5,7 +5,8 @@ streaming read on gfx950 (so it is doubled here); WRITE_SIZE is taken as is. SQ_
 SQ_ACTIVE_* count quad-cycles. Values are per launch (counter sum / launches of that kernel in the pass).
 
 usage: python tools/summarize_prof.py gpurun_out [out.txt] [--traffic tools/pmc_traffic_c2.json --source NAME]
-                                     [--workload '{"series": ..., "T": ..., "p": .., "d": .., "q": .., "I": .., "smear": ..}']
+                                     [--workload '{"series": ..., "T": ..., "p": .., "d": .., "q": .., "I": .., "smear": ..,
+                                                   "fit_kernel": 0, "options": ""}']
 (--traffic adds k_cg_fit's measured HBM bytes per launch, keyed by the workload AND the sha256 of the profiled
  library spark-timeseries_amd/libsparkts_arima.so, to the record list bench.py reads for roofline.traffic; bench.py
  reports them only for the same workload and build. Default workload: bench.py's C2 run that tools/profile.sh profiles)
@@ -58,7 +59,8 @@ def main():
         i = argv.index("--source")
         source = argv[i + 1]
         del argv[i:i + 2]
-    workload = {"series": 1048576, "T": 1024, "p": 2, "d": 1, "q": 2, "I": 1, "smear": 1}
+    workload = {"series": 1048576, "T": 1024, "p": 2, "d": 1, "q": 2, "I": 1, "smear": 1, "fit_kernel": 0,
+                "options": os.environ.get("SPARKTS_OPTIONS", "")}
     if "--workload" in argv:
         import json
         i = argv.index("--workload")
