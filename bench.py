@@ -471,6 +471,10 @@ def main():
                          "traffic_model_GBps": passes_bytes / (cg_ms * 1e-3) / 1e9 if cg_ms else None,
                          "hbm_peak_GBps": HBM_PEAK_GBS,
                          "lane_utilisation": lane_util,
+                         "objective_chain_use": (s0["spec_chains"] / s0["wave_chains"]) if s0.get("wave_chains") else None,
+                         "low_util_wave_passes": s0.get("low_util_passes"),
+                         "express_pit_passes": {"f": s0.get("express_pit_passes"), "g": s0.get("express_pit_g_passes"),
+                                                "sweeps": s0.get("express_pit_sweeps")},
                          "spec_hits_per_series": s0["spec_hits"] / max(N, 1),
                          "ride_passes_per_series": s0["ride_passes"] / max(N, 1),
                          "express_series": s0["express_series"],
@@ -539,9 +543,29 @@ def run_c5(args, eng, series, N, T, total_series, world, rank, dev, barrier, dis
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = max_over_ranks(time.perf_counter() - t0, dist if world > 1 else None)
+    st = eng.stats()                      # the last search: counter sums and algorithmic flops over its 216 fits
     o = order[:N].cpu().numpy()
     found = float((o[:, 0] >= 0).mean()) if N else 1.0
     if rank == 0:
+        search_ms = st["ms_total"]
+        achieved = st["flops"] / (search_ms * 1e-3) / 1e12 if search_ms > 0 else 0.0
+        roofline = {"bound": "fp64-valu", "kernel": "k_cg_fit (+ k_hr_init, k_ar_fit) over the 216 grid fits",
+                    "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": achieved / FP64_PEAK_TFLOPS, "launch_ms": search_ms,
+                    "achieved_source": "algorithmic flops of every grid fit of the last search step (SURVEY.md 8(d): "
+                                       "U*S*ff + G*S*fg + W_HR per fit, U and G from each fit kernel's own counters, "
+                                       "summed on the device per search lane) / the search's HIP-event duration",
+                    "flops_per_step": st["flops"], "fits": st["n_series"],
+                    "U_per_fit": (st["f_passes"] + st["ride_passes"] + st["express_f_passes"] + st["spec_hits"])
+                    / max(st["n_series"], 1),
+                    "G_per_fit": (st["g_passes"] - st["ride_passes"] + st["express_g_passes"]) / max(st["n_series"], 1),
+                    "mean_n_eval_per_fit": st["n_eval"] / max(st["n_series"], 1),
+                    "series_done": st["series_done"], "express_series": st["express_series"],
+                    "express_pit_passes": st["express_pit_passes"], "traffic": None,
+                    "traffic_source": "no PMC record for C5 (216 launches per step)"}
+        cpu, parity = None, None
+        if world == 1 and args.cpu_seconds > 0:
+            cpu, parity = c5_cpu_baseline(series, o, coef, aic, T, args.smear)
         sel = {}
         for r in o[: min(N, 65536)]:
             key = f"({r[0]},{r[1]},{r[2]}){'+c' if r[3] == 1 else ''}" if r[0] >= 0 else "none"
@@ -563,12 +587,51 @@ def run_c5(args, eng, series, N, T, total_series, world, rank, dev, barrier, dis
                        "found_fraction": found, "selected_orders_top":
                            dict(sorted(sel.items(), key=lambda kv: -kv[1])[:6]),
                        "parallelism": f"series-sharded x{world}, no collective"},
-            "roofline": None,
+            "roofline": roofline,
             "roofline_note": "per grid point (flops, evaluations, MaxEval fraction): tools/grid_profile.py",
-            "cpu_baseline": None}), flush=True)
+            "parity": parity,
+            "cpu_baseline": cpu}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def c5_cpu_baseline(series, order, coef, aic, T, smear):
+    """C5 on the CPU restatement (oracle/, kind "port"): oracle.order_search over the first rows of the shard with
+    OpenMP on the lease's CPU share, then fewer rows on one core; and the parity of those rows' selections (order,
+    approxAIC and coefficients bit for bit) with the GPU search's."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    affinity = len(os.sched_getaffinity(0))
+    cores = max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or "0") or affinity, affinity, 64))
+    O.lib()
+    rows = min(series.shape[0], 128)
+    host = series[:rows].cpu().numpy()
+    O.set_threads(cores)
+    t0 = time.perf_counter()
+    o_o, c_o, a_o = O.order_search(host, 5, 2, 5, 2, smear=smear)
+    rate = rows / (time.perf_counter() - t0)
+    one = host[:4]
+    O.set_threads(1)
+    t0 = time.perf_counter()
+    O.order_search(one, 5, 2, 5, 2, smear=smear)
+    rate1 = len(one) / (time.perf_counter() - t0)
+    O.set_threads(cores)
+    g_o = order[:rows]
+    g_c = coef[:rows].cpu().numpy()
+    g_a = aic[:rows].cpu().numpy()
+    same = (g_o == o_o).all(axis=1) & (g_a.view(np.int64) == a_o.view(np.int64)) & \
+        ((g_c.view(np.int64) == c_o.view(np.int64)) | (np.isnan(g_c) & np.isnan(c_o))).all(axis=1)
+    phys = physical_cores()
+    cpu = {"value": rate, "unit": "series searched/sec", "cores": cores, "kind": "port", "value_1core": rate1,
+           "host_physical_cores": phys, "projected_all_physical_cores": rate1 * phys if phys else None,
+           "sample": f"the first {rows} series of the shard searched over the full (5, 2, 5, +-c) grid by "
+                     f"oracle.order_search (C restatement fits, {cores} OpenMP threads); value_1core: the first "
+                     f"{len(one)} on one thread; not the spark-ts JVM"}
+    parity = {"oracle_rows": rows, "bit_identical": int(same.sum()),
+              "checked": "selected (p, d, q, intercept), approxAIC and coefficients, bit for bit"}
+    return cpu, parity
 
 
 if __name__ == "__main__":

@@ -98,6 +98,11 @@ typedef struct arima_fit_stats {
     int64_t diag[6];         /* diagnostics of builds with -DSTS_TIMING; else 0                       */
     int64_t ride_passes;     /* objective requests served by gradient passes (counted in g_passes)    */
     int64_t series_done;     /* series whose result the fit kernels wrote (== n_series unless a fault dropped some) */
+    int64_t express_pit_passes;  /* express objective passes run parallel in time (all lanes on one series)   */
+    int64_t express_pit_sweeps;  /* block sweeps of the parallel-in-time passes (objective and gradient)     */
+    int64_t express_pit_g_passes;    /* express gradient passes run parallel in time                        */
+    int64_t wave_chains;         /* objective chains the bulk objective passes computed (64 x chains per pass) */
+    int64_t low_util_passes;     /* bulk wave passes that served fewer than 32 lanes                         */
 } arima_fit_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------------------- */
@@ -115,7 +120,8 @@ int         arima_synchronize(arima_handle *h);
  * "fit_pipeline" (fit contexts in rotation for *_device fits, 1..8, default 1), "host_chunk" / "host_pipeline"
  * (series per chunk and contexts of the chunked host path, default 262144 / 3), "express_blocks",
  * "grid_blocks", "search_lanes" (in-kernel scheduler and order-search concurrency), "fit_kernel" (0: k_cg_fit with
- * LDS-resident optimizer slots; 2: rounds of streaming passes, then k_cg_fit on the last series), "rounds_max",
+ * LDS-resident optimizer slots; 2: rounds of streaming passes, then k_cg_fit on the last series; 3: k_cg_fit_r, two
+ * waves per SIMD with one optimizer slot per lane in registers, rows up to cg_fit_reg_max_n), "rounds_max",
  * "rounds_tail", "rounds_pass_waves" (fit_kernel 2), "hr_grid" (k_hr_init grid), "fit_slice_bytes"
  * (differenced workspace of one slice of a large device fit), "express_ring" (express hand-offs per launch),
  * "row_pad" (doubles added to the stride of the differenced-row workspaces, whole 128-B lines, default 0). */

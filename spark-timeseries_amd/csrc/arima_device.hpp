@@ -339,6 +339,260 @@ __device__ __forceinline__ double css_row_lds(const double *row, int n,
     return css;
 }
 
+// ------------------------------------------------------------------------------------------------------
+// Objective passes of NCH points over one series in LDS with all 64 lanes of the wave (the express path's
+// objective requests, parallel in time). The CSS recursion e_t = y_t - yh_t(e_{t-1}, e_{t-2}) is serial in t,
+// but a step only needs the two previous residuals (updateMAErrors leaves e_{t-1}, e_{t-2}, e_{t-2}, ... in
+// maTerms, ARIMA.scala:544-554). Lane L owns the time block [M + L*B, M + (L+1)*B): a SWEEP recomputes every
+// block from the two residuals its left neighbour ended the previous sweep with (lane 0 from the reference's
+// zero maTerms), with the reference's operations in the reference's order. When every lane's inputs equal its
+// neighbour's outputs of the same sweep, each block was computed from the exact serial residuals (by induction
+// from lane 0), so the block values ARE the serial recursion's, bit for bit; block 0 is exact after one sweep,
+// block L after at most L + 1, so the loop ends by sweep 64 whatever the coefficients (for a stable MA part an
+// input error shrinks by ~|root|^B per block and rounds away in 2-4 sweeps). The sum of squares is then folded
+// left over t across the lanes in order, exactly as `css = css + e * e`. Every lane returns every chain's css.
+// Chains: row h of c (all lanes pass the same coefficients); nch <= NCH of them are live (the rest are skipped).
+// ------------------------------------------------------------------------------------------------------
+template <int P, int Q, int I, int NCH, int BMAX>
+__device__ __forceinline__ void css_pit_lds(const double *row, int n, const double (&c)[NCH][I + P + Q > 0 ? I + P + Q : 1],
+                                            double (&css_out)[NCH], int lane, int *sweeps_out = nullptr) {
+    constexpr int M = (P > Q ? P : Q);
+    constexpr int PA = P > 0 ? P : 1;
+    const int S = n - M;
+    const int B = S > 0 ? (S + 63) / 64 : 0;                  // <= BMAX (the caller checks)
+    const int t0 = M + lane * B;
+    int len = n - t0;
+    len = len < 0 ? 0 : (len > B ? B : len);
+    double E[NCH][BMAX];
+    double b1[NCH], b2[NCH], yh0[NCH];
+#pragma unroll
+    for (int h = 0; h < NCH; ++h) {
+        b1[h] = b2[h] = 0.0;
+        yh0[h] = 0.0 + (double)I * c[h][0];
+    }
+    int sweeps = 0;
+    for (;;) {
+        ++sweeps;
+        double yl[PA];
+#pragma unroll
+        for (int j = 0; j < PA; ++j) yl[j] = (j < P && len > 0) ? row[t0 - 1 - j] : 0.0;
+        double e1[NCH], e2[NCH];
+#pragma unroll
+        for (int h = 0; h < NCH; ++h) {
+            e1[h] = b1[h];
+            e2[h] = b2[h];
+        }
+#pragma unroll
+        for (int b = 0; b < BMAX; ++b) {
+            if (b < len) {
+                const double yi = row[t0 + b];
+#pragma unroll
+                for (int h = 0; h < NCH; ++h) {
+                    double yh = yh0[h];                                                 // ARIMA.scala:600
+#pragma unroll
+                    for (int j = 0; j < P; ++j) yh = yh + yl[j] * c[h][I + j];          // :602-605
+#pragma unroll
+                    for (int j = 0; j < Q; ++j) yh = yh + (j == 0 ? e1[h] : e2[h]) * c[h][I + P + j];   // :608-611
+                    const double e = yi - yh;                                           // :613
+                    E[h][b] = e;
+                    e2[h] = e1[h];
+                    e1[h] = e;
+                }
+                if constexpr (P > 0) {
+#pragma unroll
+                    for (int j = PA - 1; j >= 1; --j) yl[j] = yl[j - 1];
+                    yl[0] = yi;
+                }
+            }
+        }
+        // the next sweep's inputs: the left neighbour's outputs (lane 0 keeps the zero maTerms)
+        bool moved = false;
+#pragma unroll
+        for (int h = 0; h < NCH; ++h) {
+            double n1 = __shfl_up(e1[h], 1), n2 = __shfl_up(e2[h], 1);
+            if (lane == 0) n1 = n2 = 0.0;
+            moved = moved || __double_as_longlong(n1) != __double_as_longlong(b1[h]) ||
+                    __double_as_longlong(n2) != __double_as_longlong(b2[h]);
+            b1[h] = n1;
+            b2[h] = n2;
+        }
+        if (!__any(moved)) break;                                // every block computed from exact inputs
+    }
+    // css = css + e * e over t = M .. n-1 in order (ARIMA.scala:440-442): block by block, lane by lane
+    double css[NCH];
+#pragma unroll
+    for (int h = 0; h < NCH; ++h) css[h] = 0.0;
+    for (int L = 0; L < 64; ++L) {
+        if (lane == L) {
+#pragma unroll
+            for (int b = 0; b < BMAX; ++b)
+                if (b < len) {
+#pragma unroll
+                    for (int h = 0; h < NCH; ++h) css[h] = css[h] + E[h][b] * E[h][b];
+                }
+        }
+#pragma unroll
+        for (int h = 0; h < NCH; ++h) css[h] = __shfl(css[h], L);
+    }
+#pragma unroll
+    for (int h = 0; h < NCH; ++h) css_out[h] = css[h];
+    if (sweeps_out) *sweeps_out = sweeps;
+}
+
+// Gradient pass (gradientlogLikelihoodCSSARMA, ARIMA.scala:465-534) over one series in LDS with all 64 lanes,
+// parallel in time like css_pit_lds: (1) the residual recursion by block sweeps; (2) every column of dEdTheta by
+// block sweeps -- row 0 of step t is (((0 - theta_1 dE_1) - theta_2 dE_2) ...) - direct_j(t) (:492-518), where under
+// SMEAR every lag row holds the previous row 0 (one lag value per column) and under the row shift the q previous
+// row-0 values; direct_j(t) is 1 (intercept), y_{t-1-j} (AR) or e_{t-1} / e_{t-2} (MA, the exact residuals of (1));
+// (3) the left folds of sigma2 (+ e^2 / n), css and every g_j (+ dE_0j * e) over t in order, lane by lane.
+// Every lane returns css and the whole gradient (already divided by -sigma2, :532). Storage per lane: the block's
+// residuals and K columns of dEdTheta (K * BMAX doubles), so it is used for small K only.
+template <int P, int Q, int I, bool SMEAR, int BMAX>
+__device__ __forceinline__ void grad_pit_lds(const double *row, int n, const double (&c)[I + P + Q > 0 ? I + P + Q : 1],
+                                             double &css_out, double (&g_out)[I + P + Q > 0 ? I + P + Q : 1], int lane,
+                                             int *sweeps_out = nullptr) {
+    constexpr int K = I + P + Q;
+    constexpr int KA = K > 0 ? K : 1;
+    constexpr int M = (P > Q ? P : Q);
+    constexpr int PA = P > 0 ? P : 1;
+    constexpr int DR = SMEAR ? 1 : (Q > 0 ? Q : 1);       // lag values of one column that a step reads
+    const int S = n - M;
+    const int B = S > 0 ? (S + 63) / 64 : 0;
+    const int t0 = M + lane * B;
+    int len = n - t0;
+    len = len < 0 ? 0 : (len > B ? B : len);
+    const double yh0 = 0.0 + (double)I * c[0];
+    // ---- (1) residuals ----
+    double E[BMAX];
+    double b1 = 0.0, b2 = 0.0;                            // after convergence: the exact e_{t0-1}, e_{t0-2}
+    int sweeps = 0;
+    for (;;) {
+        ++sweeps;
+        double yl[PA];
+#pragma unroll
+        for (int j = 0; j < PA; ++j) yl[j] = (j < P && len > 0) ? row[t0 - 1 - j] : 0.0;
+        double e1 = b1, e2 = b2;
+#pragma unroll
+        for (int b = 0; b < BMAX; ++b) {
+            if (b < len) {
+                const double yi = row[t0 + b];
+                double yh = yh0;
+#pragma unroll
+                for (int j = 0; j < P; ++j) yh = yh + yl[j] * c[I + j];
+#pragma unroll
+                for (int j = 0; j < Q; ++j) yh = yh + (j == 0 ? e1 : e2) * c[I + P + j];
+                const double e = yi - yh;                  // :520
+                E[b] = e;
+                e2 = e1;
+                e1 = e;
+                if constexpr (P > 0) {
+#pragma unroll
+                    for (int j = PA - 1; j >= 1; --j) yl[j] = yl[j - 1];
+                    yl[0] = yi;
+                }
+            }
+        }
+        double n1 = __shfl_up(e1, 1), n2 = __shfl_up(e2, 1);
+        if (lane == 0) n1 = n2 = 0.0;
+        const bool moved = __double_as_longlong(n1) != __double_as_longlong(b1) ||
+                           __double_as_longlong(n2) != __double_as_longlong(b2);
+        b1 = n1;
+        b2 = n2;
+        if (!__any(moved)) break;
+    }
+    // ---- (2) dEdTheta, every column ----
+    double D[KA][BMAX];
+    double bd[KA][DR];                                   // the column's lag values entering the block
+#pragma unroll
+    for (int j = 0; j < KA; ++j)
+#pragma unroll
+        for (int r = 0; r < DR; ++r) bd[j][r] = 0.0;
+    for (;;) {
+        ++sweeps;
+        double yl[PA];
+#pragma unroll
+        for (int j = 0; j < PA; ++j) yl[j] = (j < P && len > 0) ? row[t0 - 1 - j] : 0.0;
+        double e1 = b1, e2 = b2;
+        double dl[KA][DR];
+#pragma unroll
+        for (int j = 0; j < KA; ++j)
+#pragma unroll
+            for (int r = 0; r < DR; ++r) dl[j][r] = bd[j][r];
+#pragma unroll
+        for (int b = 0; b < BMAX; ++b) {
+            if (b < len) {
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    double d = 0.0;
+#pragma unroll
+                    for (int kk = 0; kk < Q; ++kk) d = d - c[I + P + kk] * dl[j][SMEAR ? 0 : kk];   // :492-499
+                    // the column's direct term (:503, :506-510, :514-518); "- I" on column 0 for I = 0 is "- 0.0",
+                    // an identity, so one subtraction per column is exact
+                    double dv;
+                    if (I && j == 0) dv = 1.0;
+                    else if (j < I + P) dv = yl[(j - I >= 0 && j - I < PA) ? j - I : 0];
+                    else dv = (j == I + P) ? e1 : e2;
+                    d = d - dv;
+                    D[j][b] = d;
+                    if constexpr (Q > 0) {                                                 // :526 (this column)
+                        if constexpr (!SMEAR) {
+#pragma unroll
+                            for (int r = DR - 1; r >= 1; --r) dl[j][r] = dl[j][r - 1];
+                        }
+                        dl[j][0] = d;
+                    }
+                }
+                const double e = E[b];
+                e2 = e1;
+                e1 = e;
+                if constexpr (P > 0) {
+#pragma unroll
+                    for (int j = PA - 1; j >= 1; --j) yl[j] = yl[j - 1];
+                    yl[0] = row[t0 + b];
+                }
+            }
+        }
+        bool moved = false;
+#pragma unroll
+        for (int j = 0; j < KA; ++j)
+#pragma unroll
+            for (int r = 0; r < DR; ++r) {
+                double v = __shfl_up(dl[j][r], 1);
+                if (lane == 0) v = 0.0;
+                moved = moved || __double_as_longlong(v) != __double_as_longlong(bd[j][r]);
+                bd[j][r] = v;
+            }
+        if (Q == 0 || !__any(moved)) break;                 // no MA part: the columns do not recur
+    }
+    // ---- (3) left folds over t in order, lane by lane ----
+    const double nd = (double)n;
+    double sigma2 = 0.0, css = 0.0, g[KA];
+#pragma unroll
+    for (int j = 0; j < KA; ++j) g[j] = 0.0;
+    for (int L = 0; L < 64; ++L) {
+        if (lane == L) {
+#pragma unroll
+            for (int b = 0; b < BMAX; ++b)
+                if (b < len) {
+                    const double e = E[b];
+                    const double e_sq = e * e;
+                    sigma2 = sigma2 + e_sq / nd;                                           // :521
+                    css = css + e_sq;
+#pragma unroll
+                    for (int j = 0; j < K; ++j) g[j] = g[j] + D[j][b] * e;                 // :524
+                }
+        }
+        sigma2 = __shfl(sigma2, L);
+        css = __shfl(css, L);
+#pragma unroll
+        for (int j = 0; j < KA; ++j) g[j] = __shfl(g[j], L);
+    }
+    css_out = css;
+#pragma unroll
+    for (int j = 0; j < KA; ++j) g_out[j] = g[j] / -sigma2;                                // :532
+    if (sweeps_out) *sweeps_out = sweeps;
+}
+
 template <int P, int Q, int I, bool SMEAR>
 __device__ __forceinline__ void grad_column_lds(const double *row, int n,
                                                 const double (&c)[I + P + Q > 0 ? I + P + Q : 1], int col,

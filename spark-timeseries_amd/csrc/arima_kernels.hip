@@ -632,6 +632,20 @@ int launch_cg_fit(const double *y, int64_t ld, int n, int64_t N, int p, int q, i
 #undef C_
 }
 
+int cg_fit_reg_max_n(int k) {
+#if !STS_REG_KERNEL
+    (void)k;
+    return -1;                                   // not built: every fit keeps k_cg_fit
+#else
+    switch (k) {
+#define K_(KK) case KK: return express_max_n<KK>(reg_wave_lds_bytes<KK>());
+        K_(1) K_(2) K_(3) K_(4) K_(5) K_(6) K_(7) K_(8) K_(9) K_(10) K_(11)
+#undef K_
+    default: return 0;
+    }
+#endif
+}
+
 int cg_fit_series_per_block(int p, int q, int I, int variant) {
 #define C_(PP) cg_fit_series_per_block_P<PP>(q, I, variant)
     STS_P_SWITCH(C_)

@@ -367,7 +367,17 @@ __device__ __forceinline__ void record_fault(unsigned long long *ctl, unsigned l
 }
 
 
-template <int P, int Q, int I, bool SMEAR>
+#ifndef STS_PIT
+#define STS_PIT 1
+#endif
+constexpr bool kPit = STS_PIT != 0;          // express objective passes parallel in time (css_pit_lds)
+
+#ifndef STS_PIT_G
+#define STS_PIT_G 1
+#endif
+constexpr int kPitGMaxK = 6;                 // gradient passes parallel in time for K <= this (K x 16 doubles per lane)
+
+template <int P, int Q, int I, bool SMEAR, int PIT_BMAX = 16, bool PIT_G = STS_PIT_G != 0>
 __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__restrict__ y, int64_t ld, int n,
                             double *__restrict__ coef_out, double *__restrict__ ll_out,
                             int32_t *__restrict__ status_out, int32_t *__restrict__ n_eval_out,
@@ -393,7 +403,8 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
     FitSlotCore<K> &ES = *reinterpret_cast<FitSlotCore<K> *>(gbase);
     double *row = reinterpret_cast<double *>(gbase + express_state_bytes<K>());
     double *xch = row + ((n + 1) & ~1);                     // K + NS + 1 doubles
-    unsigned long long served = 0, pf = 0, pg = 0, evals = 0, grads = 0, hits = 0, done = 0;
+    unsigned long long served = 0, pf = 0, pg = 0, evals = 0, grads = 0, hits = 0, done = 0, pf_pit = 0, pg_pit = 0,
+                       pit_sw = 0;
     // group state: 0 = waiting on ticket, 1 = fitting, 2 = retired (wave-uniform per group after each shfl)
     int gstate = 0;
     unsigned long long ticket = 0;
@@ -506,9 +517,68 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
             for (int j = 0; j < K; ++j) c[j] = 0.0;
         }
         const double *prow = gstate == 1 ? row : reinterpret_cast<double *>(lds + express_state_bytes<K>());
-        double cssv, gj = 0.0;
-        if (__any(req == REQ_G)) grad_column_lds<P, Q, I, SMEAR>(prow, n, c, gl < K ? gl : 0, cssv, gj);
-        else cssv = css_row_lds<P, Q, I>(prow, n, c);
+        double cssv = 0.0, gj = 0.0;
+        // one series on the whole wave: objective passes parallel in time (every lane evaluates every chain)
+        constexpr int M = (P > Q ? P : Q);
+        const bool pit = kPit && XG == 1 && req == REQ_F && n - M <= 64 * PIT_BMAX;
+        if (pit) {
+            double cm[NS + 1][K];
+            ES.s.request_point(cm[0]);
+#pragma unroll
+            for (int h = 1; h <= NS; ++h) {
+                if (h <= nsp) {
+                    ES.s.spec_point(h - 1, cm[h]);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < K; ++j) cm[h][j] = cm[0][j];
+                }
+            }
+            auto run = [&](auto NCHc, auto BMc) {
+                constexpr int NCH = decltype(NCHc)::value, BM = decltype(BMc)::value;
+                double cc[NCH][K], cs[NCH];
+#pragma unroll
+                for (int h = 0; h < NCH; ++h)
+#pragma unroll
+                    for (int j = 0; j < K; ++j) cc[h][j] = cm[h][j];
+                int sw = 0;
+                css_pit_lds<P, Q, I, NCH, BM>(prow, n, cc, cs, lane, &sw);
+                pit_sw += glead ? (unsigned long long)sw : 0ull;
+#pragma unroll
+                for (int h = 0; h < NCH; ++h)
+                    if (gl == h) cssv = cs[h];
+            };
+            auto by_b = [&](auto NCHc) {
+                if (PIT_BMAX > 16 && n - M > 64 * 16) run(NCHc, IC<(PIT_BMAX > 16 ? PIT_BMAX : 16)>{});
+                else run(NCHc, IC<16>{});
+            };
+            if constexpr (NS >= 2) {
+                if (nsp >= 2) by_b(IC<3>{});
+                else if (nsp == 1) by_b(IC<2>{});
+                else by_b(IC<1>{});
+            } else if constexpr (NS == 1) {
+                if (nsp >= 1) by_b(IC<2>{});
+                else by_b(IC<1>{});
+            } else {
+                by_b(IC<1>{});
+            }
+            pf_pit += glead;
+        } else if (PIT_G && K <= kPitGMaxK && kPit && XG == 1 && req == REQ_G && n - M <= 64 * 16) {
+            // the gradient pass parallel in time (every lane gets the whole gradient and css)
+            double cg[K], gg[K], cs = 0.0;
+            ES.s.request_point(cg);
+            int sw = 0;
+            if constexpr (K <= kPitGMaxK) grad_pit_lds<P, Q, I, SMEAR, 16>(prow, n, cg, cs, gg, lane, &sw);
+            cssv = cs;
+#pragma unroll
+            for (int j = 0; j < K; ++j)
+                if (gl == j) gj = gg[j];
+            pg_pit += glead;
+            pit_sw += glead ? (unsigned long long)sw : 0ull;
+        } else if (__any(req == REQ_G)) {
+            grad_column_lds<P, Q, I, SMEAR>(prow, n, c, gl < K ? gl : 0, cssv, gj);
+        } else {
+            cssv = css_row_lds<P, Q, I>(prow, n, c);
+        }
         if (req == REQ_F && gl <= nsp) xch[gl] = css_to_loglik(cssv, n);
         if (req == REQ_G && gl < K) xch[gl] = gj;
         if (req == REQ_G && glead) xch[K] = css_to_loglik(cssv, n);
@@ -571,6 +641,9 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
         atomicAdd(&ctl[23], served);
         atomicAdd(&ctl[24], pf);
         atomicAdd(&ctl[25], pg);
+        atomicAdd(&ctl[33], pf_pit);
+        atomicAdd(&ctl[34], pit_sw);
+        atomicAdd(&ctl[35], pg_pit);
     }
 }
 
@@ -620,7 +693,7 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
     FitSlot<K> *ws = slots[wave];
     const unsigned long long xring = express_ring_entries(ctl);
     unsigned long long lane_f = 0, lane_g = 0, wave_f = 0, wave_g = 0, wave_m = 0, evals = 0, grads = 0, hits = 0,
-                       chains = 0, rides = 0, done = 0;
+                       chains = 0, rides = 0, done = 0, wave_chains = 0, low_passes = 0;
     unsigned round_no = 0;
     bool drained = false;                  // the batch's work counter has run out (this wave saw it)
     const bool lane0 = lane == 0;
@@ -675,19 +748,15 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
                                      n_grad_out, flags_out);
                         done++;
                     } else {
-                        double x0[K], g0[K];
+                        double x0[K];
 #pragma unroll
-                        for (int j = 0; j < K; ++j) {
-                            x0[j] = init[sid * K + j];
-                            g0[j] = 0.0;
-                        }
+                        for (int j = 0; j < K; ++j) x0[j] = init[sid * K + j];
                         S.sid = sid;
 #ifdef STS_TIMING
                         S.t_start = (double)__builtin_amdgcn_s_memrealtime();
                         S.t_donate = 0.0;
 #endif
-                        S.s.start(x0);
-                        S.s.advance(0.0, g0);           // posts the first request: G at the initial point
+                        S.s.start_posted(x0);           // posts the first request: G at the initial point
                         need = false;
                     }
                 }
@@ -835,7 +904,9 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
             if (nch > 1) wave_m += lane0; else wave_f += lane0;
             lane_f += served;
             chains += served ? (unsigned long long)(1 + nsp) : 0ull;
+            wave_chains += lane0 ? (unsigned long long)(64 * nch) : 0ull;
         }
+        low_passes += (lane0 && nsel < 32) ? 1ull : 0ull;
         // ---- each lane advances its slot with the response; finished slots are written out and refilled ----
 #ifdef STS_TIMING
         const unsigned long long t_c = now();
@@ -851,7 +922,11 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
             CGLane<K, NS, spec_nc<K>()> &L = S.s;
 #endif
             L.req = REQ_NONE;
+#if STS_ADV_REGS == 2
+            L.step(resp_f, g);                    // force-inlined on the register copy (A/B)
+#else
             L.advance(resp_f, g);
+#endif
             if (L.done()) {
                 double pt[K];
 #pragma unroll
@@ -986,11 +1061,21 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
     atomicAdd(&ctl[9], chains);
     atomicAdd(&ctl[18], rides);
     atomicAdd(&ctl[32], done);
+    if (lane0) {
+        atomicAdd(&ctl[36], wave_chains);       // chains the objective passes computed (64 lanes x NCH each)
+        atomicAdd(&ctl[37], low_passes);        // wave passes that served fewer than 32 lanes
+    }
 }
 
 }  // namespace sts
 
 #include "arima_fit_rounds.hpp"
+#ifndef STS_REG_KERNEL
+#define STS_REG_KERNEL 0                     // fit_kernel 3 (k_cg_fit_r) is built only on request: measured slower
+#endif
+#if STS_REG_KERNEL
+#include "arima_fit_reg.hpp"
+#endif
 
 namespace sts {
 
@@ -1139,6 +1224,20 @@ int launch_cg_fit_PS(const double *y, int64_t ld, int n, int64_t N, int q, int I
                     return ARIMA_E_INVALID_ARG;
                 } else {
                     constexpr int SPW = fit_slots_per_wave<K>();
+#if STS_REG_KERNEL
+                    if (variant == 3) {                   // two waves per SIMD, register slots (arima_fit_reg.hpp)
+                        constexpr int SPL = reg_lds_slots<K>();
+                        if (n > express_max_n<K>(reg_wave_lds_bytes<K>())) express_blocks = 0;
+                        hipLaunchKernelGGL((k_cg_fit_r<P, Q, II, S, SPL>), dim3(grid_blocks + express_blocks), dim3(64),
+                                           0, s, y, ld, n, N, init, init_status, coef_out, ll_out, status_out,
+                                           n_eval_out, n_grad_out, flags_out, ctl, xq, xready, grid_blocks,
+                                           join_express, nullptr, nullptr, nullptr);
+                        STS_CHECK_LAUNCH();
+                        return ARIMA_OK;
+                    }
+#else
+                    if (variant == 3) return ARIMA_E_UNSUPPORTED;
+#endif
                     // express blocks only when the row fits next to the state in one wave's LDS share
                     const int lds_per_wave = SPW * (int)sizeof(FitSlot<K>);
                     if (n > express_max_n<K>(lds_per_wave)) express_blocks = 0;
@@ -1215,6 +1314,9 @@ int cg_fit_series_per_block_P(int q, int I, int variant) {
         return with_bool(I, [&](auto Ic) {
             constexpr int Q = decltype(Qc)::value, II = decltype(Ic)::value;
             if constexpr (P + Q + II == 0) return 0;
+#if STS_REG_KERNEL
+            else if (variant == 3) return 64 + reg_lds_slots<P + Q + II>();
+#endif
             else return kFitWaves * fit_slots_per_wave<P + Q + II>();
         });
     });

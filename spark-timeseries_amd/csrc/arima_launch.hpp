@@ -81,6 +81,12 @@ constexpr int kFitBlockWaves = STS_FIT_BLOCK_WAVES;   // waves per k_cg_fit work
 constexpr int kFitWavesPerCU = STS_FIT_WAVES_PER_CU;  // resident k_cg_fit waves per CU (4: one per SIMD)
 constexpr int kFitBlocksPerCU = kFitWavesPerCU / kFitBlockWaves;
 
+// fit_kernel = 3 (k_cg_fit_r, arima_fit_reg.hpp): two single-wave workgroups per SIMD, one optimizer slot per lane in
+// registers plus a reserve in the wave's eighth of the LDS. Its express waves stage rows of at most
+// cg_fit_reg_max_n(k) doubles; longer rows keep k_cg_fit (variant 0).
+constexpr int kRegWavesPerCU = 8;
+int cg_fit_reg_max_n(int k);
+
 int hr_shape_status_host(int n, int p, int q, int I);
 int ar_shape_status_host(int n, int p, int I);
 

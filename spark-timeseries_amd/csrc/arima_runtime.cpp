@@ -76,6 +76,7 @@ struct SearchLane {
     FitWs ws;
     DevBuf coef, ll, status, neval, ngrad, flags;
     DevBuf best_aic, best_order, best_coef;    // this lane's best candidate per series (merged at the end)
+    DevBuf acc;                                // kCtlWords counter sums over the lane's fits + their flops (double)
 };
 
 // A device fit larger than one slice (option "fit_slice_bytes" of differenced workspace; default 0 = 60 % of the free
@@ -167,6 +168,9 @@ struct arima_handle {
     hipEvent_t ev_diff[kMaxD + 1] = {};
     SearchLane lanes[kMaxSearchLanes];
     DevBuf os_order;
+    unsigned long long *search_acc_host = nullptr;   // pinned: (kCtlWords + 1) words per lane of the last search
+    int search_lanes_used = 0;
+    int64_t search_n = 0, search_fits = 0;
 };
 
 namespace {
@@ -217,6 +221,25 @@ __global__ void k_fault_take(unsigned long long *__restrict__ rec) {
     const unsigned long long code = atomicExch(&rec[0], 0ull);
     rec[8] = code;
     for (int i = 1; i < 6; ++i) rec[8 + i] = code ? atomicExch(&rec[i], 0ull) : 0ull;
+}
+
+// One grid point's fit into its search lane's counter sums (order-search stats, arima_get_last_stats): every kernel
+// counter word, and the fit's algorithmic flops by compute_stats' formula. cg = 0: the AR-only
+// shortcut or a uniform status (no counters; every series written).
+__global__ void k_search_acc(const unsigned long long *__restrict__ ctl, unsigned long long *__restrict__ acc,
+                             int64_t N, int n, int p, int q, int I, int cg) {
+    if (threadIdx.x != 0) return;
+    for (int i = 0; i < 40; ++i) acc[i] += ctl[i];
+    if (!cg) acc[32] += (unsigned long long)N;
+    const int k = I + p + q, M = p > q ? p : q, m = M + 1;
+    const double S = n - M > 0 ? n - M : 0;
+    const double ff = 2.0 * (p + q) + 4, fg = ff + 2.0 * k * q + 1 + p + q + 2.0 * k;
+    const double U = (double)(ctl[1] + ctl[18] + ctl[24] + ctl[7]), G = (double)(ctl[2] - ctl[18] + ctl[25]);
+    const double whr = (double)N * (3.0 * (n - m > 0 ? n - m : 0) * (m + 1) * (m + 1) +
+                                    3.0 * (n - 2 * M - 1 > 0 ? n - 2 * M - 1 : 0) * k * k +
+                                    2.0 * (n - m > 0 ? n - m : 0) * m);
+    double *fl = reinterpret_cast<double *>(acc + 40);
+    *fl = *fl + U * S * ff + G * S * fg + whr;
 }
 
 // the first watchdog fault of a fit kernel (its ctl[26..31]) into the handle's sticky device record
@@ -285,6 +308,9 @@ int arima_create(int device, arima_handle **out) {
     if (rc == ARIMA_OK &&
         hipHostMalloc((void **)&h->slot_ctl, (size_t)kSliceSlots * kCtlWords * sizeof(unsigned long long), 0) != hipSuccess)
         rc = ARIMA_E_OOM;
+    if (rc == ARIMA_OK && hipHostMalloc((void **)&h->search_acc_host,
+                                        (size_t)kMaxSearchLanes * (kCtlWords + 1) * sizeof(unsigned long long), 0) != hipSuccess)
+        rc = ARIMA_E_OOM;
     if (rc == ARIMA_OK && h->dev_fault.ensure(16 * sizeof(unsigned long long)) != ARIMA_OK) rc = ARIMA_E_OOM;
     if (rc == ARIMA_OK && hipMemset(h->dev_fault.ptr, 0, 16 * sizeof(unsigned long long)) != hipSuccess) rc = ARIMA_E_DEVICE;
     if (rc != ARIMA_OK) {
@@ -325,6 +351,7 @@ int arima_destroy(arima_handle *h) {
         for (auto &e : sl.ev)
             if (e) hipEventDestroy(e);
     if (h->slot_ctl) hipHostFree(h->slot_ctl);
+    if (h->search_acc_host) hipHostFree(h->search_acc_host);
     for (auto &e : h->ev)
         if (e) hipEventDestroy(e);
     if (h->ev_done) hipEventDestroy(h->ev_done);
@@ -360,6 +387,46 @@ int arima_get_last_stats(const arima_handle *hc, arima_fit_stats *out) {
         h->stats = acc;
         h->slice_n = 0;
         h->slice_acc = arima_fit_stats{};
+    } else if (h->stats_ctx == -3 && h->search_lanes_used > 0) {   // an order search: the sums over its fits
+        hipSetDevice(h->device);
+        if (hipEventSynchronize(h->ev[4]) != hipSuccess) return set_err(h, ARIMA_E_DEVICE, "stats: device error");
+        arima_fit_stats st{};
+        double flops = 0.0;
+        unsigned long long w[kCtlWords] = {};
+        for (int j = 0; j < h->search_lanes_used; ++j) {
+            const unsigned long long *a = h->search_acc_host + (size_t)j * (kCtlWords + 1);
+            for (int i = 0; i < kCtlWords; ++i) w[i] += a[i];
+            double f;
+            memcpy(&f, a + kCtlWords, sizeof f);
+            flops += f;
+        }
+        st.n_series = h->search_n * h->search_fits;          // fits (series x grid points)
+        st.f_passes = (int64_t)w[1];
+        st.g_passes = (int64_t)w[2];
+        st.wave_f_passes = (int64_t)w[3];
+        st.wave_g_passes = (int64_t)w[4];
+        st.n_eval = (int64_t)w[5];
+        st.n_grad = (int64_t)w[6];
+        st.spec_hits = (int64_t)w[7];
+        st.wave_multi_passes = (int64_t)w[8];
+        st.spec_chains = (int64_t)w[9];
+        st.ride_passes = (int64_t)w[18];
+        st.express_series = (int64_t)w[23];
+        st.express_f_passes = (int64_t)w[24];
+        st.express_g_passes = (int64_t)w[25];
+        st.series_done = (int64_t)w[32];
+        st.express_pit_passes = (int64_t)w[33];
+        st.express_pit_sweeps = (int64_t)w[34];
+        st.express_pit_g_passes = (int64_t)w[35];
+        st.wave_chains = (int64_t)w[36];
+        st.low_util_passes = (int64_t)w[37];
+        st.flops = flops;
+        float ms = 0;
+        hipEventElapsedTime(&ms, h->ev[0], h->ev[3]);
+        st.ms_cg_fit = ms;
+        st.ms_total = ms;
+        h->stats = st;
+        h->search_lanes_used = 0;
     }
     *out = h->stats;
     return ARIMA_OK;
@@ -416,7 +483,9 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
     std::lock_guard<std::mutex> lk(h->mu);
     if (!strcmp(name, "smear")) { h->smear = value ? 1 : 0; return ARIMA_OK; }
     if (!strcmp(name, "fit_kernel")) {
-        if (value != 0 && value != 2) return set_err(h, ARIMA_E_INVALID_ARG, "fit_kernel: 0 or 2");
+        if (value != 0 && value != 2 && value != 3) return set_err(h, ARIMA_E_INVALID_ARG, "fit_kernel: 0, 2 or 3");
+        if (value == 3 && sts::cg_fit_reg_max_n(1) < 0)
+            return set_err(h, ARIMA_E_UNSUPPORTED, "fit_kernel 3: built only with -DSTS_REG_KERNEL=1");
         h->fit_kernel = (int)value;
         return ARIMA_OK;
     }
@@ -568,8 +637,9 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
     if (xcus >= cus) xcus = cus - 1;
     int bcus = h->grid_blocks_override;
     if (bcus <= 0) bcus = std::max(1, cus - xcus);
-    const int variant = h->fit_kernel;
-    const int bpc = sts::kFitBlocksPerCU;
+    // fit_kernel 3 (two waves per SIMD) where its express waves can stage the rows, else k_cg_fit
+    const int variant = (h->fit_kernel == 3 && n > sts::cg_fit_reg_max_n(k)) ? 0 : h->fit_kernel;
+    const int bpc = variant == 3 ? sts::kRegWavesPerCU : sts::kFitBlocksPerCU;
     int xblocks = xcus * bpc;
     int blocks = bcus * bpc;
     const int per_block = std::max(1, sts::cg_fit_series_per_block(p, q, I, variant));
@@ -719,6 +789,11 @@ static arima_fit_stats compute_stats(const PendingStats &ps, const unsigned long
     st.express_series = (int64_t)cc[23];
     st.express_f_passes = (int64_t)cc[24];
     st.express_g_passes = (int64_t)cc[25];
+    st.express_pit_passes = (int64_t)cc[33];
+    st.express_pit_sweeps = (int64_t)cc[34];
+    st.express_pit_g_passes = (int64_t)cc[35];
+    st.wave_chains = (int64_t)cc[36];
+    st.low_util_passes = (int64_t)cc[37];
     st.express_blocks = ps.express;
     st.fault = (int64_t)cc[26];
     for (int i = 0; i < 5; ++i) st.fault_info[i] = (int64_t)cc[27 + i];
@@ -882,6 +957,11 @@ static void acc_stats(arima_fit_stats &a, const arima_fit_stats &s) {
     a.express_series += s.express_series;
     a.express_f_passes += s.express_f_passes;
     a.express_g_passes += s.express_g_passes;
+    a.express_pit_passes += s.express_pit_passes;
+    a.express_pit_sweeps += s.express_pit_sweeps;
+    a.express_pit_g_passes += s.express_pit_g_passes;
+    a.wave_chains += s.wave_chains;
+    a.low_util_passes += s.low_util_passes;
     a.grid_blocks = s.grid_blocks;
     a.express_blocks = s.express_blocks;
     if (!a.fault && s.fault) {
@@ -1251,6 +1331,7 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
         if (rc == ARIMA_OK) rc = ln.best_order.ensure((size_t)N * 4 * sizeof(int32_t));
         if (rc == ARIMA_OK) rc = ln.best_coef.ensure((size_t)N * 11 * sizeof(double));
         if (rc == ARIMA_OK) rc = ln.ws.ctl.ensure(kCtlWords * sizeof(unsigned long long));
+        if (rc == ARIMA_OK) rc = ln.acc.ensure((kCtlWords + 1) * sizeof(unsigned long long));
         if (rc == ARIMA_OK) rc = ln.ws.xring.ensure(sts::kExpressRingBytes);
         if (rc == ARIMA_OK) rc = ln.ws.xready.ensure(sts::kExpressReadyBytes);
         if (rc == ARIMA_OK && h->fit_kernel == 2) rc = ensure_rounds_ws(h, ln.ws, N, 11);
@@ -1287,6 +1368,7 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
         HIPCHK(h, hipStreamWaitEvent(ln.stream, h->ev[0], 0));
         RCCHK(h, sts::launch_search_init(ln.best_aic.as<double>(), ln.best_order.as<int32_t>(),
                                          ln.best_coef.as<double>(), N, ln.stream), "search_init");
+        HIPCHK(h, hipMemsetAsync(ln.acc.ptr, 0, (kCtlWords + 1) * sizeof(unsigned long long), ln.stream));
     }
     const int i_lo = intercept_mode == 1 ? 1 : 0, i_hi = intercept_mode == 0 ? 0 : 1;
     struct GridPoint { int d, p, q, I; double cost; };
@@ -1336,6 +1418,10 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
                                      ln.coef.as<double>(), ln.ll.as<double>(), ln.status.as<int32_t>(),
                                      ln.neval.as<int32_t>(), ln.ngrad.as<int32_t>(), ln.flags.as<uint8_t>(), ln.stream,
                                      nullptr, &gridb, &xb, L > 1), "fit");
+                hipLaunchKernelGGL(k_search_acc, dim3(1), dim3(64), 0, ln.stream, ln.ws.ctl.as<unsigned long long>(),
+                                   ln.acc.as<unsigned long long>(), N, n, p, q, I,
+                                   (p > 0 && q == 0) || method != ARIMA_METHOD_CSS_CGD || I + p + q == 0 ? 0 : 1);
+                HIPCHK(h, hipGetLastError());
                 // a fit whose kernel recorded a watchdog fault contributes nothing (its outputs are incomplete) and
                 // the fault reaches the caller through the handle's sticky record (arima_synchronize)
                 RCCHK(h, sts::launch_search_select(ln.coef.as<double>(), ln.ll.as<double>(), ln.status.as<int32_t>(),
@@ -1357,6 +1443,14 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
     }
     RCCHK(h, sts::launch_search_merge(bests, L, N, d_aic, d_order, d_coef, s), "search_merge");
     HIPCHK(h, hipEventRecord(h->ev[3], s));
+    for (int j = 0; j < L; ++j)                    // the lanes' counter sums, read by arima_get_last_stats
+        HIPCHK(h, hipMemcpyAsync(h->search_acc_host + (size_t)j * (kCtlWords + 1), h->lanes[j].acc.ptr,
+                                 (kCtlWords + 1) * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipEventRecord(h->ev[4], s));
+    h->stats_ctx = -3;
+    h->search_lanes_used = L;
+    h->search_n = N;
+    h->search_fits = fits;
     if (n_fits) *n_fits = fits;
     return ARIMA_OK;
 }

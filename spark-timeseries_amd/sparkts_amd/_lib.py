@@ -62,7 +62,10 @@ class FitStats(ctypes.Structure):
                 ("express_blocks", ctypes.c_int64), ("express_series", ctypes.c_int64),
                 ("express_f_passes", ctypes.c_int64), ("express_g_passes", ctypes.c_int64),
                 ("fault", ctypes.c_int64), ("fault_info", ctypes.c_int64 * 5),
-                ("diag", ctypes.c_int64 * 6), ("ride_passes", ctypes.c_int64), ("series_done", ctypes.c_int64)]
+                ("diag", ctypes.c_int64 * 6), ("ride_passes", ctypes.c_int64), ("series_done", ctypes.c_int64),
+                ("express_pit_passes", ctypes.c_int64), ("express_pit_sweeps", ctypes.c_int64),
+                ("express_pit_g_passes", ctypes.c_int64), ("wave_chains", ctypes.c_int64),
+                ("low_util_passes", ctypes.c_int64)]
 
     def as_dict(self):
         d = {name: getattr(self, name) for name, _ in self._fields_}

@@ -410,6 +410,27 @@ def test_long_fits_through_express(engine):
     assert st["express_series"] > 0, st
 
 
+@pytest.mark.parametrize("name", ["c4_515_T512", "c1_101_T500", "c2_212_T1024_shift", "grid_p5d0q5i1", "grid_p1d2q4i0",
+                                  "grid_p0d1q3i1", "grid_p3d0q1i0", "edge_nan_101", "kat_ds1_101_userinit"])
+def test_express_objective_passes_parallel_in_time(engine, name):
+    # express waves evaluate objective requests with all 64 lanes on one series (css_pit_lds: blocks of the time
+    # axis swept until every block's inputs equal its left neighbour's outputs, then the sum of squares folded in
+    # order): bit-identical to the oracle's serial recursion. A small batch drains the work counter at once, so
+    # fits longer than 32 evaluations are donated to the express path.
+    meta, arr = load_case(name)
+    engine.set_option("smear", meta["smear"])
+    try:
+        res = engine.fit_batch(arr["series"], meta["p"], meta["d"], meta["q"], meta["I"], meta["method"],
+                               arr.get("user_init"))
+        st = engine.stats()
+    finally:
+        engine.set_option("smear", L.DEFAULT_SMEAR)
+    check_fit(res, arr, name)
+    if name == "c4_515_T512":
+        assert st["express_pit_passes"] > 0, st
+        assert st["express_pit_sweeps"] >= 2 * st["express_pit_passes"], st
+
+
 def test_host_path_chunks_match_oracle(engine):
     # arima_fit_batch cut into 7 chunks over 3 fit contexts (uploads overlapping earlier chunks' fits): every
     # series bit-identical to the oracle, and the counters summed over the chunks
