@@ -103,6 +103,8 @@ typedef struct arima_fit_stats {
     int64_t express_pit_g_passes;    /* express gradient passes run parallel in time                        */
     int64_t wave_chains;         /* objective chains the bulk objective passes computed (64 x chains per pass) */
     int64_t low_util_passes;     /* bulk wave passes that served fewer than 32 lanes                         */
+    int64_t diag_step_cycles;    /* STS_TIMING builds: optimizer-step cycles, and refill cycles (within diag[2]) */
+    int64_t diag_refill_cycles;
 } arima_fit_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------------------- */

@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "../../include/sparkts_arima.h"
 #include "cg_lane.hpp"
 
@@ -446,7 +448,7 @@ __device__ __forceinline__ void css_pit_lds(const double *row, int n, const doub
 // row-0 values; direct_j(t) is 1 (intercept), y_{t-1-j} (AR) or e_{t-1} / e_{t-2} (MA, the exact residuals of (1));
 // (3) the left folds of sigma2 (+ e^2 / n), css and every g_j (+ dE_0j * e) over t in order, lane by lane.
 // Every lane returns css and the whole gradient (already divided by -sigma2, :532). Storage per lane: the block's
-// residuals and K columns of dEdTheta (K * BMAX doubles), so it is used for small K only.
+// residuals and up to 6 columns of dEdTheta at a time (K > 6: two column chunks, each swept and folded in turn).
 template <int P, int Q, int I, bool SMEAR, int BMAX>
 __device__ __forceinline__ void grad_pit_lds(const double *row, int n, const double (&c)[I + P + Q > 0 ? I + P + Q : 1],
                                              double &css_out, double (&g_out)[I + P + Q > 0 ? I + P + Q : 1], int lane,
@@ -500,93 +502,105 @@ __device__ __forceinline__ void grad_pit_lds(const double *row, int n, const dou
         b2 = n2;
         if (!__any(moved)) break;
     }
-    // ---- (2) dEdTheta, every column ----
-    double D[KA][BMAX];
-    double bd[KA][DR];                                   // the column's lag values entering the block
-#pragma unroll
-    for (int j = 0; j < KA; ++j)
-#pragma unroll
-        for (int r = 0; r < DR; ++r) bd[j][r] = 0.0;
-    for (;;) {
-        ++sweeps;
-        double yl[PA];
-#pragma unroll
-        for (int j = 0; j < PA; ++j) yl[j] = (j < P && len > 0) ? row[t0 - 1 - j] : 0.0;
-        double e1 = b1, e2 = b2;
-        double dl[KA][DR];
-#pragma unroll
-        for (int j = 0; j < KA; ++j)
-#pragma unroll
-            for (int r = 0; r < DR; ++r) dl[j][r] = bd[j][r];
-#pragma unroll
-        for (int b = 0; b < BMAX; ++b) {
-            if (b < len) {
-#pragma unroll
-                for (int j = 0; j < K; ++j) {
-                    double d = 0.0;
-#pragma unroll
-                    for (int kk = 0; kk < Q; ++kk) d = d - c[I + P + kk] * dl[j][SMEAR ? 0 : kk];   // :492-499
-                    // the column's direct term (:503, :506-510, :514-518); "- I" on column 0 for I = 0 is "- 0.0",
-                    // an identity, so one subtraction per column is exact
-                    double dv;
-                    if (I && j == 0) dv = 1.0;
-                    else if (j < I + P) dv = yl[(j - I >= 0 && j - I < PA) ? j - I : 0];
-                    else dv = (j == I + P) ? e1 : e2;
-                    d = d - dv;
-                    D[j][b] = d;
-                    if constexpr (Q > 0) {                                                 // :526 (this column)
-                        if constexpr (!SMEAR) {
-#pragma unroll
-                            for (int r = DR - 1; r >= 1; --r) dl[j][r] = dl[j][r - 1];
-                        }
-                        dl[j][0] = d;
-                    }
-                }
-                const double e = E[b];
-                e2 = e1;
-                e1 = e;
-                if constexpr (P > 0) {
-#pragma unroll
-                    for (int j = PA - 1; j >= 1; --j) yl[j] = yl[j - 1];
-                    yl[0] = row[t0 + b];
-                }
-            }
-        }
-        bool moved = false;
-#pragma unroll
-        for (int j = 0; j < KA; ++j)
-#pragma unroll
-            for (int r = 0; r < DR; ++r) {
-                double v = __shfl_up(dl[j][r], 1);
-                if (lane == 0) v = 0.0;
-                moved = moved || __double_as_longlong(v) != __double_as_longlong(bd[j][r]);
-                bd[j][r] = v;
-            }
-        if (Q == 0 || !__any(moved)) break;                 // no MA part: the columns do not recur
-    }
-    // ---- (3) left folds over t in order, lane by lane ----
+    // ---- (2) + (3) per chunk of at most 6 columns of dEdTheta (K * BMAX doubles would not fit the registers) ----
+    constexpr int KC = K <= 6 ? KA : 6;
     const double nd = (double)n;
     double sigma2 = 0.0, css = 0.0, g[KA];
 #pragma unroll
     for (int j = 0; j < KA; ++j) g[j] = 0.0;
-    for (int L = 0; L < 64; ++L) {
-        if (lane == L) {
+    auto chunk = [&](auto J0c) {
+        constexpr int J0 = decltype(J0c)::value;
+        constexpr int JN = (J0 + KC < K ? J0 + KC : K) - J0;      // columns J0 .. J0 + JN - 1
+        double D[KC][BMAX];
+        double bd[KC][DR];                                       // a column's lag values entering the block
 #pragma unroll
-            for (int b = 0; b < BMAX; ++b)
+        for (int jj = 0; jj < KC; ++jj)
+#pragma unroll
+            for (int r = 0; r < DR; ++r) bd[jj][r] = 0.0;
+        for (;;) {
+            ++sweeps;
+            double yl[PA];
+#pragma unroll
+            for (int j = 0; j < PA; ++j) yl[j] = (j < P && len > 0) ? row[t0 - 1 - j] : 0.0;
+            double e1 = b1, e2 = b2;
+            double dl[KC][DR];
+#pragma unroll
+            for (int jj = 0; jj < KC; ++jj)
+#pragma unroll
+                for (int r = 0; r < DR; ++r) dl[jj][r] = bd[jj][r];
+#pragma unroll
+            for (int b = 0; b < BMAX; ++b) {
                 if (b < len) {
+#pragma unroll
+                    for (int jj = 0; jj < JN; ++jj) {
+                        const int j = J0 + jj;
+                        double d = 0.0;
+#pragma unroll
+                        for (int kk = 0; kk < Q; ++kk) d = d - c[I + P + kk] * dl[jj][SMEAR ? 0 : kk];   // :492-499
+                        // the column's direct term (:503, :506-510, :514-518); "- I" on column 0 for I = 0 is
+                        // "- 0.0", an identity, so one subtraction per column is exact
+                        double dv;
+                        if (I && j == 0) dv = 1.0;
+                        else if (j < I + P) dv = yl[(j - I >= 0 && j - I < PA) ? j - I : 0];
+                        else dv = (j == I + P) ? e1 : e2;
+                        d = d - dv;
+                        D[jj][b] = d;
+                        if constexpr (Q > 0) {                                             // :526 (this column)
+                            if constexpr (!SMEAR) {
+#pragma unroll
+                                for (int r = DR - 1; r >= 1; --r) dl[jj][r] = dl[jj][r - 1];
+                            }
+                            dl[jj][0] = d;
+                        }
+                    }
                     const double e = E[b];
-                    const double e_sq = e * e;
-                    sigma2 = sigma2 + e_sq / nd;                                           // :521
-                    css = css + e_sq;
+                    e2 = e1;
+                    e1 = e;
+                    if constexpr (P > 0) {
 #pragma unroll
-                    for (int j = 0; j < K; ++j) g[j] = g[j] + D[j][b] * e;                 // :524
+                        for (int j = PA - 1; j >= 1; --j) yl[j] = yl[j - 1];
+                        yl[0] = row[t0 + b];
+                    }
                 }
-        }
-        sigma2 = __shfl(sigma2, L);
-        css = __shfl(css, L);
+            }
+            bool moved = false;
 #pragma unroll
-        for (int j = 0; j < KA; ++j) g[j] = __shfl(g[j], L);
-    }
+            for (int jj = 0; jj < JN; ++jj)
+#pragma unroll
+                for (int r = 0; r < DR; ++r) {
+                    double v = __shfl_up(dl[jj][r], 1);
+                    if (lane == 0) v = 0.0;
+                    moved = moved || __double_as_longlong(v) != __double_as_longlong(bd[jj][r]);
+                    bd[jj][r] = v;
+                }
+            if (Q == 0 || !__any(moved)) break;                 // no MA part: the columns do not recur
+        }
+        // (3) left folds over t in order, lane by lane: sigma2 and css with the first chunk, this chunk's g_j
+        for (int L = 0; L < 64; ++L) {
+            if (lane == L) {
+#pragma unroll
+                for (int b = 0; b < BMAX; ++b)
+                    if (b < len) {
+                        const double e = E[b];
+                        if constexpr (J0 == 0) {
+                            const double e_sq = e * e;
+                            sigma2 = sigma2 + e_sq / nd;                                   // :521
+                            css = css + e_sq;
+                        }
+#pragma unroll
+                        for (int jj = 0; jj < JN; ++jj) g[J0 + jj] = g[J0 + jj] + D[jj][b] * e;   // :524
+                    }
+            }
+            if constexpr (J0 == 0) {
+                sigma2 = __shfl(sigma2, L);
+                css = __shfl(css, L);
+            }
+#pragma unroll
+            for (int jj = 0; jj < JN; ++jj) g[J0 + jj] = __shfl(g[J0 + jj], L);
+        }
+    };
+    if constexpr (K > 0) chunk(std::integral_constant<int, 0>{});
+    if constexpr (K > KC) chunk(std::integral_constant<int, KC>{});
     css_out = css;
 #pragma unroll
     for (int j = 0; j < KA; ++j) g_out[j] = g[j] / -sigma2;                                // :532

@@ -375,7 +375,7 @@ constexpr bool kPit = STS_PIT != 0;          // express objective passes paralle
 #ifndef STS_PIT_G
 #define STS_PIT_G 1
 #endif
-constexpr int kPitGMaxK = 6;                 // gradient passes parallel in time for K <= this (K x 16 doubles per lane)
+constexpr int kPitGMaxK = 12;                // gradient passes parallel in time (in column chunks of 6) for K <= this
 
 template <int P, int Q, int I, bool SMEAR, int PIT_BMAX = 16, bool PIT_G = STS_PIT_G != 0>
 __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__restrict__ y, int64_t ld, int n,
@@ -700,7 +700,7 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
 #ifdef STS_TIMING
     // diagnostics build only: shader-clock cycles per phase, summed over waves (ctl[10..13]), the kernel span
     // (ctl[14] = max end, ctl[15] = min start) and the per-wave time after the batch drained (ctl[16])
-    unsigned long long tm_f = 0, tm_g = 0, tm_adv = 0, tm_sel = 0, tm_drain = 0;
+    unsigned long long tm_f = 0, tm_g = 0, tm_adv = 0, tm_sel = 0, tm_drain = 0, tm_step = 0, tm_refill = 0;
     const unsigned long long tm_start = __builtin_amdgcn_s_memtime();
     auto now = [] { return __builtin_amdgcn_s_memtime(); };
 #endif
@@ -945,7 +945,14 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
             S.s = L;
 #endif
         }
+#ifdef STS_TIMING
+        const unsigned long long t_s = now();
+        tm_step += t_s - t_c;
+#endif
         refill(my, need);
+#ifdef STS_TIMING
+        tm_refill += now() - t_s;
+#endif
         if (has_express) {
             // an express wave is waiting: hand it this wave's oldest slot (the likely critical path)
             unsigned long long wants = 0, filled = 0, fault = 0;
@@ -1046,6 +1053,8 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
         atomicMax(&ctl[14], tm_end);
         atomicMin(&ctl[15], tm_start);
         atomicAdd(&ctl[16], tm_drain ? tm_end - tm_drain : 0ull);
+        atomicAdd(&ctl[38], tm_step);              // (part of tm_adv) the served slots' optimizer steps
+        atomicAdd(&ctl[39], tm_refill);            // (part of tm_adv) refills from the work counter
     }
 #endif
     atomicAdd(&ctl[1], lane_f);

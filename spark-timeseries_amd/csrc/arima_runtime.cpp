@@ -794,6 +794,8 @@ static arima_fit_stats compute_stats(const PendingStats &ps, const unsigned long
     st.express_pit_g_passes = (int64_t)cc[35];
     st.wave_chains = (int64_t)cc[36];
     st.low_util_passes = (int64_t)cc[37];
+    st.diag_step_cycles = (int64_t)cc[38];
+    st.diag_refill_cycles = (int64_t)cc[39];
     st.express_blocks = ps.express;
     st.fault = (int64_t)cc[26];
     for (int i = 0; i < 5; ++i) st.fault_info[i] = (int64_t)cc[27 + i];

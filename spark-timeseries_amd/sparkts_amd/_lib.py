@@ -65,7 +65,8 @@ class FitStats(ctypes.Structure):
                 ("diag", ctypes.c_int64 * 6), ("ride_passes", ctypes.c_int64), ("series_done", ctypes.c_int64),
                 ("express_pit_passes", ctypes.c_int64), ("express_pit_sweeps", ctypes.c_int64),
                 ("express_pit_g_passes", ctypes.c_int64), ("wave_chains", ctypes.c_int64),
-                ("low_util_passes", ctypes.c_int64)]
+                ("low_util_passes", ctypes.c_int64), ("diag_step_cycles", ctypes.c_int64),
+                ("diag_refill_cycles", ctypes.c_int64)]
 
     def as_dict(self):
         d = {name: getattr(self, name) for name, _ in self._fields_}

@@ -59,6 +59,10 @@ def main():
             "phase_frac": {"f": dg[0] / tot, "g": dg[1] / tot, "adv": dg[2] / tot, "sel": dg[3] / tot} if tot else None,
             "cyc_per_step_f_any": dg[0] / max(wf + wm, 1) / S, "cyc_per_step_g": dg[1] / max(wg, 1) / S,
             "cyc_adv_per_pass": dg[2] / max(wp, 1), "cyc_sel_per_pass": dg[3] / max(wp, 1),
+            "cyc_step_per_pass": st.get("diag_step_cycles", 0) / max(wp, 1),
+            "cyc_refill_per_pass": st.get("diag_refill_cycles", 0) / max(wp, 1),
+            "objective_chain_use": st["spec_chains"] / st["wave_chains"] if st.get("wave_chains") else None,
+            "low_util_passes": st.get("low_util_passes"),
             "drained_Mcyc_per_wave": dg[5] / max(st["grid_blocks"], 1) / 1e6,
             "n_eval": st["n_eval"], "series_done": st["series_done"]}), flush=True)
 
