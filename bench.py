@@ -478,6 +478,7 @@ def main():
                          "spec_hits_per_series": s0["spec_hits"] / max(N, 1),
                          "ride_passes_per_series": s0["ride_passes"] / max(N, 1),
                          "express_series": s0["express_series"],
+                         "merge": {"series": s0.get("merge_series"), "waves": s0.get("merge_waves")},
                          "wave_passes": {"f": s0["wave_f_passes"], "g": s0["wave_g_passes"],
                                          "multi": s0["wave_multi_passes"]}},
             "cpu_baseline": None,
@@ -561,7 +562,10 @@ def run_c5(args, eng, series, N, T, total_series, world, rank, dev, barrier, dis
                     "G_per_fit": (st["g_passes"] - st["ride_passes"] + st["express_g_passes"]) / max(st["n_series"], 1),
                     "mean_n_eval_per_fit": st["n_eval"] / max(st["n_series"], 1),
                     "series_done": st["series_done"], "express_series": st["express_series"],
-                    "express_pit_passes": st["express_pit_passes"], "traffic": None,
+                    "express_pit_passes": st["express_pit_passes"],
+                    "express_wave_passes": st["express_f_passes"] + st["express_g_passes"],
+                    "bulk_wave_passes": st["wave_f_passes"] + st["wave_g_passes"] + st["wave_multi_passes"],
+                    "merge": {"series": st.get("merge_series"), "waves": st.get("merge_waves")}, "traffic": None,
                     "traffic_source": "no PMC record for C5 (216 launches per step)"}
         cpu, parity = None, None
         if world == 1 and args.cpu_seconds > 0:

@@ -92,7 +92,7 @@ typedef struct arima_fit_stats {
     int64_t express_series;  /* series finished on the express path                                    */
     int64_t express_f_passes; /* objective / gradient passes run on the express path                    */
     int64_t express_g_passes;
-    int64_t fault;           /* != 0: the fit kernel's hand-off watchdog fired (1 = stall, 2 = lost request);
+    int64_t fault;           /* != 0: the fit kernel's hand-off watchdog fired (1 = stall, 2 = lost request, 3 = merge stall);
                                 the call also returns ARIMA_E_DEVICE from arima_synchronize / blocking entry points */
     int64_t fault_info[5];   /* the kernel's record of the first fault (ticket, fills, bulk waves done, ...)      */
     int64_t diag[6];         /* diagnostics of builds with -DSTS_TIMING; else 0                       */
@@ -105,6 +105,8 @@ typedef struct arima_fit_stats {
     int64_t low_util_passes;     /* bulk wave passes that served fewer than 32 lanes                         */
     int64_t diag_step_cycles;    /* STS_TIMING builds: optimizer-step cycles, and refill cycles (within diag[2]) */
     int64_t diag_refill_cycles;
+    int64_t merge_series;        /* series the drain merge moved between bulk waves (option "merge_live")    */
+    int64_t merge_waves;         /* bulk waves that handed their last series over and left                   */
 } arima_fit_stats;
 
 /* ---- lifecycle ------------------------------------------------------------------------------------- */
@@ -126,7 +128,9 @@ int         arima_synchronize(arima_handle *h);
  * waves per SIMD with one optimizer slot per lane in registers, rows up to cg_fit_reg_max_n), "rounds_max",
  * "rounds_tail", "rounds_pass_waves" (fit_kernel 2), "hr_grid" (k_hr_init grid), "fit_slice_bytes"
  * (differenced workspace of one slice of a large device fit), "express_ring" (express hand-offs per launch),
- * "row_pad" (doubles added to the stride of the differenced-row workspaces, whole 128-B lines, default 0). */
+ * "row_pad" (doubles added to the stride of the differenced-row workspaces, whole 128-B lines, default 0),
+ * "merge_live" (k_cg_fit drain merge: after the batch's work counter ran out, a wave with at most this many live
+ * series hands them to waves still running and exits, 0..64, 0 = off; results never depend on it). */
 int         arima_set_option(arima_handle *h, const char *name, int64_t value);
 /* Current value of a tuning knob (the names arima_set_option takes); ARIMA_E_INVALID_ARG for an unknown name. */
 int         arima_get_option(const arima_handle *h, const char *name, int64_t *value);

@@ -216,6 +216,14 @@ constexpr bool kFRide = STS_F_RIDE != 0;     // objective requests fill the idle
 #define STS_OLD_EVALS 128
 #endif
 constexpr int kOldEvals = STS_OLD_EVALS;     // evaluations after which a series is served with priority
+#ifndef STS_NCH_CHOICE
+#define STS_NCH_CHOICE 1
+#endif
+constexpr bool kNchChoice = STS_NCH_CHOICE != 0;   // objective pass width chosen by evaluations per cost
+#ifndef STS_CHAIN_OVERHEAD16
+#define STS_CHAIN_OVERHEAD16 6
+#endif
+constexpr int kChainOverhead16 = STS_CHAIN_OVERHEAD16;   // per-step streaming cost of a pass, in 1/16 chains
 #ifndef STS_ADV_REGS
 #define STS_ADV_REGS 0                       // bulk optimizer steps on a register copy of the LDS slot (A/B: DESIGN 7.2)
 #endif
@@ -282,9 +290,12 @@ constexpr int kExpressTagWord = kExpressEntryBytes / 8 - 1;
 // ring entries this launch may fill: ctl[19] when the host set it (option "express_ring", tests reach the cap with a
 // small ring), else the whole ring. Tickets beyond it are never filled (their groups retire); their series stay on
 // the bulk path, so reaching the cap changes where a series is fitted, never its result.
+// With the drain merge on (ctl[44] > 0) the ring's upper half is the merge pool, so hand-offs stop at its lower half.
+constexpr int kMergeCap = kExpressRing / 2;  // merge pool entries per launch (never reused within it)
 __device__ __forceinline__ unsigned long long express_ring_entries(const unsigned long long *ctl) {
     const unsigned long long r = ctl[19];
-    return (r == 0 || r > (unsigned long long)kExpressRing) ? (unsigned long long)kExpressRing : r;
+    const unsigned long long cap = ctl[44] ? (unsigned long long)(kExpressRing - kMergeCap) : (unsigned long long)kExpressRing;
+    return (r == 0 || r > cap) ? cap : r;
 }
 
 // Every word shared between workgroups of a launch is accessed as a GLOBAL (address space 1) agent-scope access,
@@ -352,7 +363,7 @@ constexpr int express_group_bytes(int n) { return express_state_bytes<K>() + ((n
 // posts no request without being finished is dropped; either records the first fault in ctl[26..31] (the host
 // reports it as a device error) and the wave drains normally.
 constexpr unsigned long long kWatchdogTicks = 2000000000ull;    // 20 s without any progress of the launch
-enum : unsigned long long { FAULT_HANDOFF_STALL = 1, FAULT_NO_REQUEST = 2 };
+enum : unsigned long long { FAULT_HANDOFF_STALL = 1, FAULT_NO_REQUEST = 2, FAULT_MERGE_STALL = 3 };
 
 __device__ __forceinline__ void record_fault(unsigned long long *ctl, unsigned long long code, unsigned long long a,
                                              unsigned long long b, unsigned long long c, unsigned long long d,
@@ -690,6 +701,20 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+    // Drain merge (round 4; ctl[44] = merge_live > 0, set by the host): once the batch's work counter has run out,
+    // a wave whose live slots dropped to merge_live or fewer hands them to the merge pool (the upper half of the
+    // express ring) and leaves; waves still running take pool entries into their free slots (up to 64 live). Few
+    // waves then run nearly full passes instead of many nearly empty ones, and a leaving wave's SIMD (its whole
+    // workgroup, once all four left) goes to the next fit sharing the GPU. ctl[40] = active waves (bits 0-23) |
+    // entries reserved (bits 24-63), ctl[41] = entries claimed, ctl[42] = waves that handed over, ctl[43] = claims.
+    // A wave reserves entries and leaves the active count in one CAS, and leaves without entries only by a CAS that
+    // sees every reserved entry claimed -- so while entries are unclaimed some active wave remains to take them.
+    // Only where a series is fitted changes, never its result.
+    const int merge_live = resume_list ? 0 : (int)ctl[44];
+    unsigned char *mpool = xq + (size_t)(kExpressRing - kMergeCap) * kExpressEntryBytes;
+    unsigned *mready = xready + (kExpressRing - kMergeCap);
+    unsigned long long merge_head = 0;     // entries claimed, as last seen (a lower bound)
+    if (merge_live > 0 && lane == 0) add_agent(&ctl[40], 1ull);
     FitSlot<K> *ws = slots[wave];
     const unsigned long long xring = express_ring_entries(ctl);
     unsigned long long lane_f = 0, lane_g = 0, wave_f = 0, wave_g = 0, wave_m = 0, evals = 0, grads = 0, hits = 0,
@@ -778,50 +803,215 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
         // Long-running series (>= kOldEvals evaluations) set the critical path of the launch, so their requests
         // choose the pass type and are served first; the other slots are taken in a rotating order (no slot
         // starves while more than 64 requests of its type are pending).
-        unsigned long long mF[NJ], mG[NJ], mO[NJ];
-        int nF = 0, nG = 0, nOF = 0, nOG = 0;
+        unsigned long long mF[NJ], mG[NJ], mO[NJ], mP1[NJ], mP2[NJ];
+        int nF = 0, nG = 0, nOF = 0, nOG = 0, nP1 = 0, nP2 = 0;
 #pragma unroll
         for (int j = 0; j < NJ; ++j) {
             const int slot = lane + 64 * j;
-            int r = REQ_NONE;
+            int r = REQ_NONE, nsp_j = 0;
             bool old = false;
             if (slot < SPW && ws[slot].c.sid >= 0) {
                 r = ws[slot].c.s.req;
                 old = ws[slot].c.s.n_eval >= kOldEvals;
+                nsp_j = ws[slot].c.s.rq_nspec;
             }
             mF[j] = __ballot(r == REQ_F);
             mG[j] = __ballot(r == REQ_G);
             mO[j] = __ballot(old);
+            mP1[j] = __ballot(r == REQ_F && nsp_j >= 1);
+            mP2[j] = __ballot(r == REQ_F && nsp_j >= 2);
             nF += __popcll(mF[j]);
             nG += __popcll(mG[j]);
             nOF += __popcll(mF[j] & mO[j]);
             nOG += __popcll(mG[j] & mO[j]);
+            nP1 += __popcll(mP1[j]);
+            nP2 += __popcll(mP2[j]);
+        }
+        if (merge_live > 0 && __any(drained)) {
+            const int live = nF + nG;
+            int occ = 0;                          // occupied slots (live ones, with a request posted, in practice)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) occ += __popcll(__ballot(lane + 64 * j < SPW && ws[lane + 64 * j].c.sid >= 0));
+            constexpr int kRoom = SPW < 64 ? SPW : 64;
+            int act = 0;                          // 1 = handed over, 2 = claimed entries, 3 = left (pool empty)
+            unsigned long long mbase = 0, mcnt = 0;
+            if (lane0) {
+                unsigned long long w = rd_fresh(&ctl[40]);
+                bool offer = live > 0 && live <= merge_live;
+                for (;;) {
+                    const unsigned long long active = w & 0xffffffull, tail = w >> 24;
+                    if (offer) {
+                        if (active > 1 && tail + (unsigned long long)live <= (unsigned long long)kMergeCap) {
+                            const unsigned long long o = cas_agent(&ctl[40], w, ((tail + live) << 24) | (active - 1));
+                            if (o == w) {
+                                act = 1;
+                                mbase = tail;
+                                break;
+                            }
+                            w = o;
+                            continue;
+                        }
+                        offer = false;            // nobody left to take them, or the pool is full: keep fitting
+                    }
+                    if (occ < kRoom && tail > merge_head) {
+                        unsigned long long head = rd_fresh(&ctl[41]);
+                        while (head < tail) {
+                            const unsigned long long c = tail - head < (unsigned long long)(kRoom - occ)
+                                                             ? tail - head : (unsigned long long)(kRoom - occ);
+                            const unsigned long long o = cas_agent(&ctl[41], head, head + c);
+                            if (o == head) {
+                                act = 2;
+                                mbase = head;
+                                mcnt = c;
+                                break;
+                            }
+                            head = o;
+                        }
+                        merge_head = act == 2 ? mbase + mcnt : head;
+                        if (act == 2) break;
+                    }
+                    if (live > 0) break;
+                    // nothing live and every reserved entry claimed: leave (fails if an entry was reserved meanwhile)
+                    const unsigned long long o = cas_agent(&ctl[40], w, w - 1ull);
+                    if (o == w) {
+                        act = 3;
+                        break;
+                    }
+                    w = o;
+                }
+            }
+            act = __shfl(act, 0);
+            if (act == 1) {                       // every live slot into entries mbase.. in slot order
+                mbase = __shfl(mbase, 0);
+                int rk = 0;
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    const unsigned long long m = mF[j] | mG[j];
+                    const int slot = lane + 64 * j;
+                    if ((m >> lane) & 1ull) {
+                        const unsigned long long e = mbase + (unsigned long long)(rk + __popcll(m & ((1ull << lane) - 1ull)));
+                        constexpr int W = (int)(sizeof(FitSlotCore<K>) / 8);
+                        unsigned long long *dst = reinterpret_cast<unsigned long long *>(mpool + (size_t)e * kExpressEntryBytes);
+                        const unsigned long long *src = reinterpret_cast<const unsigned long long *>(&ws[slot].c);
+                        for (int w = 0; w < W; ++w) st_agent(&dst[w], src[w]);
+                        st_agent(&dst[kExpressTagWord], e + 1ull);
+                    }
+                    rk += __popcll(m);
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the entries before their ready words
+                rk = 0;
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    const unsigned long long m = mF[j] | mG[j];
+                    const int slot = lane + 64 * j;
+                    if ((m >> lane) & 1ull) {
+                        const unsigned long long e = mbase + (unsigned long long)(rk + __popcll(m & ((1ull << lane) - 1ull)));
+                        st_agent(&mready[e], (unsigned)(e + 1ull));
+                        ws[slot].c.sid = -1;
+                        ws[slot].c.s.req = REQ_NONE;
+                    }
+                    rk += __popcll(m);
+                }
+                if (lane0) add_agent(&ctl[42], 1ull);
+                break;
+            }
+            if (act == 3) break;
+            if (act == 2) {                       // entries mbase .. mbase + mcnt - 1 into the free slots, in order
+                mbase = __shfl(mbase, 0);
+                mcnt = __shfl(mcnt, 0);
+                int rk = 0;
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    const int slot = lane + 64 * j;
+                    const bool fr = slot < SPW && ws[slot].c.sid < 0;
+                    const unsigned long long m = __ballot(fr);
+                    const int r = rk + __popcll(m & ((1ull << lane) - 1ull));
+                    if (fr && (unsigned long long)r < mcnt) {
+                        const unsigned long long e = mbase + (unsigned long long)r;
+                        const unsigned long long *src =
+                            reinterpret_cast<const unsigned long long *>(mpool + (size_t)e * kExpressEntryBytes);
+                        unsigned long long t0 = 0;
+                        bool ok = true;
+                        while (!(rd_fresh(&mready[e]) == (unsigned)(e + 1ull) && rd_fresh(&src[kExpressTagWord]) == e + 1ull)) {
+                            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+                            if (t0 == 0) {
+                                t0 = t;
+                            } else if (t - t0 > kWatchdogTicks) {   // never spin forever: the series is reported lost
+                                record_fault(ctl, FAULT_MERGE_STALL, e, ld_agent(&ctl[40]), ld_agent(&ctl[41]), 0, 0);
+                                ok = false;
+                                break;
+                            }
+                            __builtin_amdgcn_s_sleep(2);
+                        }
+                        if (ok) {
+                            constexpr int W = (int)(sizeof(FitSlotCore<K>) / 8);
+                            unsigned long long *dst = reinterpret_cast<unsigned long long *>(&ws[slot].c);
+                            for (int w = 0; w < W; ++w) dst[w] = rd_fresh(&src[w]);
+                        }
+                    }
+                    rk += __popcll(m);
+                }
+                if (lane0) add_agent(&ctl[43], 1ull);
+                wave_sync_lds();
+                continue;
+            }
         }
         if (nF + nG == 0) break;                  // batch drained and every slot of this wave finished
         // (round 3: a cost-aware choice -- G when min(64, nG + nF) per gradient-pass cost beats min(64, nF) per
         // objective-pass cost -- measured at weights 2-4: C2 and C4 unchanged within noise, profiles/r03/o_gw)
         const bool doG = nOG != nOF ? nOG > nOF : (nG >= 64 || (nF < 64 && nG >= nF));
+        // Objective pass width (round 4): an objective pass runs NCH chains on every lane, so a lane whose request
+        // carries fewer predictions than NCH - 1 pays for chains it does not use. Choose NCH for the most objective
+        // evaluations per unit of pass cost (cost ~ NCH + the per-step streaming share, kChainOverhead16 / 16 of a
+        // chain), serving up to 64 requests, those that use all NCH chains first. Requests whose extra predictions
+        // do not fit are served without them (a prediction only fills the value cache; results are unchanged).
+        int nchc = NS + 1;
+        if (kNchChoice && !doG) {
+            const int n2 = nP2, n1 = nP1 - nP2, n0 = nF - nP1;
+            int best = -1;
+#pragma unroll
+            for (int c = 1; c <= NS + 1; ++c) {
+                int left = 64, u = 0, t;
+                t = n2 < left ? n2 : left; u += t * (c < 3 ? c : 3); left -= t;
+                t = n1 < left ? n1 : left; u += t * (c < 2 ? c : 2); left -= t;
+                t = n0 < left ? n0 : left; u += t; left -= t;
+                const int score = u * 4096 / (kChainOverhead16 + 16 * c);
+                if (score >= best) { best = score; nchc = c; }
+            }
+        }
         const int rot = (int)(round_no * 37u) & 63;
         round_no++;
         // A gradient pass also yields the objective, so its lanes left over after the G requests serve objective
-        // requests (tiers 2-3: the request's own point; its predicted points wait for an objective pass).
+        // requests (tiers 2-3: the request's own point; its predicted points wait for an objective pass). An
+        // objective pass serves long-running requests first, then those that use all nchc chains, then the rest.
         int base = 0;
 #pragma unroll
-        for (int tier = 0; tier < (kFRide ? 4 : 2); ++tier) {
-            if (tier >= 2 && (!doG || base >= 64)) break;
+        for (int tier = 0; tier < 4; ++tier) {
+            if (tier >= 2 && ((doG && !kFRide) || (!doG && !kNchChoice) || base >= 64)) break;
+            if (tier == 3 && !doG) break;
 #pragma unroll
             for (int jj = 0; jj < NJ; ++jj) {
                 const int j = (jj + (int)round_no) % NJ;
                 // select the slot group's masks without a dynamically indexed register array (that would live in
                 // scratch memory: 4 scratch loads per pass selection)
-                unsigned long long wG = mG[0], wF = mF[0], wO = mO[0];
+                unsigned long long wG = mG[0], wF = mF[0], wO = mO[0], wP1 = mP1[0], wP2 = mP2[0];
 #pragma unroll
                 for (int i = 1; i < NJ; ++i) {
                     wG = (j == i) ? mG[i] : wG;
                     wF = (j == i) ? mF[i] : wF;
                     wO = (j == i) ? mO[i] : wO;
+                    wP1 = (j == i) ? mP1[i] : wP1;
+                    wP2 = (j == i) ? mP2[i] : wP2;
                 }
-                unsigned long long m = ((doG && tier < 2) ? wG : wF) & ((tier & 1) == 0 ? wO : ~wO);
+                unsigned long long m;
+                if (doG) {
+                    m = (tier < 2 ? wG : wF) & ((tier & 1) == 0 ? wO : ~wO);
+                } else if (!kNchChoice) {
+                    m = wF & (tier == 0 ? wO : ~wO);
+                } else {
+                    const unsigned long long full = nchc >= 3 ? wP2 : (nchc == 2 ? wP1 : ~0ull);
+                    m = wF & (tier == 0 ? wO : (tier == 1 ? (~wO & full) : (~wO & ~full)));
+                }
                 m = (m >> rot) | (rot ? (m << (64 - rot)) : 0ull);          // rotate: lane rot ranks first
                 const int lr = (lane - rot) & 63;
                 if ((m >> lr) & 1ull) {
@@ -859,8 +1049,10 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
             lane_g += served;
             rides += (served && S.s.req == REQ_F) ? 1ull : 0ull;
         } else {
-            // chains = 1 + the most predictions any served lane posted (wave-uniform)
-            const int nsp = served ? (int)S.s.rq_nspec : 0;
+            // chains = 1 + the most predictions any served lane posted, at most the chosen width (wave-uniform);
+            // a lane evaluates its first nch - 1 predictions
+            int nsp = served ? (int)S.s.rq_nspec : 0;
+            nsp = nsp < nchc - 1 ? nsp : nchc - 1;
             int nch = 1;
 #pragma unroll
             for (int h = 1; h <= NS; ++h)

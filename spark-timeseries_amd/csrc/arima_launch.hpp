@@ -85,6 +85,9 @@ constexpr int kFitBlocksPerCU = kFitWavesPerCU / kFitBlockWaves;
 // registers plus a reserve in the wave's eighth of the LDS. Its express waves stage rows of at most
 // cg_fit_reg_max_n(k) doubles; longer rows keep k_cg_fit (variant 0).
 constexpr int kRegWavesPerCU = 8;
+#ifndef STS_MERGE_LIVE_DEFAULT
+#define STS_MERGE_LIVE_DEFAULT 16            // k_cg_fit's drain merge threshold (option "merge_live"; 0 = off)
+#endif
 int cg_fit_reg_max_n(int k);
 
 int hr_shape_status_host(int n, int p, int q, int I);

@@ -47,7 +47,7 @@ struct DevBuf {
 };
 
 constexpr int kNumEvents = 5;
-constexpr int kCtlWords = 40;     // device counters of the fit kernel (k_cg_fit's ctl[]; ctl[32] = series written)
+constexpr int kCtlWords = 48;     // device counters of the fit kernel (k_cg_fit's ctl[]; ctl[32] = series written)
 
 // What arima_get_last_stats needs to turn the device counters of the last fit into arima_fit_stats. The fit
 // entry points do not wait for the device (the `*_device` contract): the counters are copied to pinned host
@@ -133,6 +133,7 @@ struct arima_handle {
     int grid_blocks_override = 0;
     int express_blocks = -1;       // k_cg_fit express workgroups (-1: num_cus / 16)
     int express_ring = 0;          // express hand-offs per launch (0: the whole ring, sts::kExpressRingEntries)
+    int merge_live = STS_MERGE_LIVE_DEFAULT;   // k_cg_fit drain merge: hand over at <= this many live slots (0: off)
     int hr_grid = 0;               // k_hr_init: 0 = a lane per series; > 0 = that many single-wave workgroups
     int row_pad = 0;               // doubles (multiple of 16) added to the differenced rows' stride
     int fit_kernel = 0;            // 0: k_cg_fit (LDS slots, 1 wave/SIMD); 2: rounds of streaming passes + k_cg_fit
@@ -229,7 +230,7 @@ __global__ void k_fault_take(unsigned long long *__restrict__ rec) {
 __global__ void k_search_acc(const unsigned long long *__restrict__ ctl, unsigned long long *__restrict__ acc,
                              int64_t N, int n, int p, int q, int I, int cg) {
     if (threadIdx.x != 0) return;
-    for (int i = 0; i < 40; ++i) acc[i] += ctl[i];
+    for (int i = 0; i < kCtlWords; ++i) acc[i] += ctl[i];
     if (!cg) acc[32] += (unsigned long long)N;
     const int k = I + p + q, M = p > q ? p : q, m = M + 1;
     const double S = n - M > 0 ? n - M : 0;
@@ -238,7 +239,7 @@ __global__ void k_search_acc(const unsigned long long *__restrict__ ctl, unsigne
     const double whr = (double)N * (3.0 * (n - m > 0 ? n - m : 0) * (m + 1) * (m + 1) +
                                     3.0 * (n - 2 * M - 1 > 0 ? n - 2 * M - 1 : 0) * k * k +
                                     2.0 * (n - m > 0 ? n - m : 0) * m);
-    double *fl = reinterpret_cast<double *>(acc + 40);
+    double *fl = reinterpret_cast<double *>(acc + kCtlWords);
     *fl = *fl + U * S * ff + G * S * fg + whr;
 }
 
@@ -420,6 +421,8 @@ int arima_get_last_stats(const arima_handle *hc, arima_fit_stats *out) {
         st.express_pit_g_passes = (int64_t)w[35];
         st.wave_chains = (int64_t)w[36];
         st.low_util_passes = (int64_t)w[37];
+        st.merge_series = (int64_t)w[41];
+        st.merge_waves = (int64_t)w[42];
         st.flops = flops;
         float ms = 0;
         hipEventElapsedTime(&ms, h->ev[0], h->ev[3]);
@@ -507,6 +510,7 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
         h->express_ring = (int)std::min<int64_t>(sts::kExpressRingEntries, std::max<int64_t>(0, value));
         return ARIMA_OK;
     }
+    if (!strcmp(name, "merge_live")) { h->merge_live = (int)std::min<int64_t>(64, std::max<int64_t>(0, value)); return ARIMA_OK; }
     if (!strcmp(name, "express_blocks")) { h->express_blocks = (int)std::max<int64_t>(-1, value); return ARIMA_OK; }
     if (!strcmp(name, "grid_blocks")) { h->grid_blocks_override = (int)std::max<int64_t>(0, value); return ARIMA_OK; }
     if (!strcmp(name, "search_lanes")) {
@@ -537,7 +541,7 @@ int arima_get_option(const arima_handle *hc, const char *name, int64_t *value) {
         {"fit_kernel", h->fit_kernel}, {"hr_grid", h->hr_grid}, {"row_pad", h->row_pad}, {"rounds_max", h->rounds_max},
         {"rounds_tail", h->rounds_tail}, {"rounds_pass_waves", h->rounds_pass_waves},
         {"rounds_tail_express", h->rounds_tail_express}, {"rounds_tail_cus", h->rounds_tail_cus},
-        {"rounds_tail_xcus", h->rounds_tail_xcus}};
+        {"rounds_tail_xcus", h->rounds_tail_xcus}, {"merge_live", h->merge_live}};
     for (const auto &o : opts)
         if (!strcmp(name, o.n)) {
             *value = o.v;
@@ -603,6 +607,8 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
     HIPCHK(h, hipMemsetAsync(ws.ctl.as<unsigned long long>() + 15, 0xff, sizeof(unsigned long long), s));
     if (h->express_ring > 0)                                   // ctl[19]: the launch's ring entries (low word)
         HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)(ws.ctl.as<unsigned long long>() + 19), h->express_ring, 1, s));
+    if (h->merge_live > 0)                                     // ctl[44]: k_cg_fit's drain merge threshold
+        HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)(ws.ctl.as<unsigned long long>() + 44), h->merge_live, 1, s));
     if (p > 0 && q == 0) {                                     // AR-only shortcut, method never checked
         if (ev_mid) HIPCHK(h, hipEventRecord(ev_mid, s));
         RCCHK(h, sts::launch_ar_fit(y, ldn, n, N, p, I, d_coef, d_ll, d_status, d_neval, d_ngrad, d_flags, s),
@@ -645,7 +651,7 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
     const int per_block = std::max(1, sts::cg_fit_series_per_block(p, q, I, variant));
     const int64_t need = (N + per_block - 1) / per_block;
     if (blocks > need) blocks = (int)need;
-    if (xblocks > 0) {
+    if (xblocks > 0 || h->merge_live > 0) {                   // the merge pool is the ring's upper half
         RCCHK(h, ws.xring.ensure(sts::kExpressRingBytes), "workspace");
         RCCHK(h, ws.xready.ensure(sts::kExpressReadyBytes), "workspace");
         HIPCHK(h, hipMemsetAsync(ws.xready.ptr, 0, sts::kExpressReadyBytes, s));
@@ -796,6 +802,8 @@ static arima_fit_stats compute_stats(const PendingStats &ps, const unsigned long
     st.low_util_passes = (int64_t)cc[37];
     st.diag_step_cycles = (int64_t)cc[38];
     st.diag_refill_cycles = (int64_t)cc[39];
+    st.merge_series = (int64_t)cc[41];
+    st.merge_waves = (int64_t)cc[42];
     st.express_blocks = ps.express;
     st.fault = (int64_t)cc[26];
     for (int i = 0; i < 5; ++i) st.fault_info[i] = (int64_t)cc[27 + i];
@@ -964,6 +972,8 @@ static void acc_stats(arima_fit_stats &a, const arima_fit_stats &s) {
     a.express_pit_g_passes += s.express_pit_g_passes;
     a.wave_chains += s.wave_chains;
     a.low_util_passes += s.low_util_passes;
+    a.merge_series += s.merge_series;
+    a.merge_waves += s.merge_waves;
     a.grid_blocks = s.grid_blocks;
     a.express_blocks = s.express_blocks;
     if (!a.fault && s.fault) {

@@ -303,198 +303,25 @@ struct CGLane {
     // out-of-line: the LDS-resident slots of the bulk kernel and the express path call it through a pointer
     STS_HD void advance(double fr, const double (&gr)[K]) { step(fr, gr); }
 
-    // the state machine itself, force-inlined where the lane's state is a register-resident copy.
-    // Control flow (round 4): the evaluation subroutine runs inline at its call site, and every unconditional
-    // transition (bracket f(xC) -> loop test, shift -> loop test, Brent f(mid) / f(u) -> next Brent step, line search
-    // done -> gradient -> next iteration) continues in the same trip through the loop. A wave advances 64 lanes in
-    // different states at once and pays for the union of their paths on every trip, so fewer trips per call is what
-    // counts (tests/sim: 5.7 trips per call, up to 13, before). Same operations in the same order.
+    // the state machine itself, force-inlined where the lane's state is a register-resident copy
     STS_HD STS_FI void step(double fr, const double (&gr)[K]) {
         const double GS = brent_gs();
         double ev_val = fr;                                   // objective value delivered to the resume point
         double grad[K];                                       // gradient delivered to PC_G0 / PC_G
 #pragma unroll
         for (int i = 0; i < K; ++i) grad[i] = gr[i];
-        // LineSearch's objective at point + alpha * dir (A-2 .. A-4) with the reference's accounting. Returns true when
-        // it posted an objective request (the machine waits for the response and resumes at `ret`); false when the
-        // value is already known -- f(point) memoised (the bracket's f(0), Brent's f(mid)), a non-finite point (NaN),
-        // a speculative hit -- with ev_val set and pc = ret, or when the fit failed (pc = PC_DONE).
-        auto eval = [&](double alpha, int bracket, int memo_ok, double memo, int ret) -> bool {
+        // eval subroutine (LineSearch's objective): locals of this call, never live across a pass
+        double ev_memo = 0.0;
+        int ev_memo_ok = 0, ev_bracket = 0, ev_ret = PC_DONE;
+        auto eval = [&](double alpha, int bracket, int memo_ok, double memo, int ret) {
             ev_alpha = alpha;
-            if (bracket) {
-                if (bcount + 1 > kBracketMax) { fail(ARIMA_ST_BRACKET_MAX_EVAL); return false; }
-                bcount++;
-            }
-            if (n_eval + 1 > kMaxEval) { fail(ARIMA_ST_MAX_EVAL); return false; }
-            n_eval++;
-            pc = (uint8_t)ret;                                // resume point
-            if (memo_ok) { ev_val = memo; return false; }
-            bool fin = true;
-#pragma unroll
-            for (int i = 0; i < K; ++i) fin = fin && finite(point[i] + ev_alpha * dir[i]);
-            if (!fin) { ev_val = __builtin_nan(""); return false; }
-            if constexpr (NC > 0) {
-                const long long ab = dbits(ev_alpha);
-                bool hit = false;
-#pragma unroll
-                for (int s = 0; s < NC; ++s)
-                    if (s < sp_n && dbits(sp_alpha[s]) == ab) { ev_val = sp_f[s]; hit = true; }
-                if (hit) { spec_hits++; return false; }
-            }
-            rq_nspec = (uint8_t)predict(ret);
-            req = REQ_F;
-            return true;
-        };
-        // top of the CG loop (iterations.increment, F(point), convergence, line search start)
-        auto top = [&]() -> bool {
-            if constexpr (FF) {
-                // NaN-absorbing state: a non-finite coordinate makes every later evaluation NaN
-                // (point + alpha * dir is never finite), and with F(point) = NaN the convergence test is false, so
-                // the reference runs kNanIterEvals evaluations per iteration (one gradient each, at the end) until
-                // MaxEval. Jump there: the m iterations that still fit complete, the next one stops inside with
-                // MAX_EVAL at n_eval = kMaxEval (iter <= n_eval / 2, so MaxIter cannot come first). Failed fits
-                // report NaN coefficients, so the point itself no longer matters.
-                bool pfin = true;
-#pragma unroll
-                for (int i = 0; i < K; ++i) pfin = pfin && finite(point[i]);
-                if (!pfin && __builtin_isnan(memo_obj)) {
-                    const int m = (kMaxEval - (int)n_eval) / kNanIterEvals;
-                    n_grad = (uint16_t)(n_grad + m);
-                    iter = (uint16_t)(iter + m + 1);
-                    n_eval = (uint16_t)kMaxEval;
-                    fail(ARIMA_ST_MAX_EVAL);
-                    return false;
-                }
-            }
-            if (iter + 1 > kMaxIter) { fail(ARIMA_ST_MAX_ITER); return false; }
-            iter++;
-            if (n_eval + 1 > kMaxEval) { fail(ARIMA_ST_MAX_EVAL); return false; }
-            n_eval++;
-            const double objective = memo_obj;
-            const bool conv = have_prev_obj && value_converged(prev_obj, objective, 1e-7, 1e-7);
-            prev_obj = objective;
-            have_prev_obj = 1;
-            if (conv) { pc = PC_DONE; return false; }   // status OK; point / prev_obj are the result
-            // line.search(point, searchDirection)
-            sp_n = sp_next = 0;
-            bcount = 0;
-            xA = 0.0;
-            xB = 1e-8;
-            bool dfin = true;
-#pragma unroll
-            for (int i = 0; i < K; ++i) dfin = dfin && finite(dir[i]);
-            return eval(xA, 1, dfin ? 1 : 0, objective, PC_BR_FA);
-        };
-        // bracket -> Brent (shared storage: read everything needed before writing)
-        auto br_end = [&]() -> bool {
-            double lo = xA, hi = xC;
-            const double mid = xB, fmid = fB;
-            if (lo > hi) { double t = lo; lo = hi; hi = t; }
-            if (lo >= hi || mid < lo || mid > hi) { fail(ARIMA_ST_BAD_INTERVAL); return false; }  // SearchInterval
-            if (lo < hi) { a = lo; b = hi; } else { a = hi; b = lo; }
-            bx = bv = bw = mid;
-            bd = be = 0.0;
-            return eval(mid, 0, 1, fmid, PC_BRENT_FX);                   // fx = f(mid) (memo: bracket fMid)
-        };
-        // BracketFinder's loop test and its next point
-        auto br_loop = [&]() -> bool {
-            if (!(fC > fB)) return br_end();
-            const double tmp1 = (xB - xA) * (fB - fC);
-            const double tmp2 = (xB - xC) * (fB - fA);
-            const double val = tmp2 - tmp1;
-            const double denom = dabs(val) < kEpsMin ? 2 * kEpsMin : val;
-            w = xB - ((xB - xC) * tmp2 - (xB - xA) * tmp1) / (2 * denom);
-            const double wLim = xB + kGrow * (xC - xB);
-            if ((w - xC) * (xB - w) > 0) return eval(w, 1, 0, 0.0, PC_BR_A1);
-            if ((w - wLim) * (wLim - xC) >= 0) {
-                w = wLim;
-                return eval(w, 1, 0, 0.0, PC_BR_SHIFT_EV);
-            }
-            if ((w - wLim) * (xC - w) > 0) return eval(w, 1, 0, 0.0, PC_BR_C1);
-            w = xC + kGold * (xC - xB);
-            return eval(w, 1, 0, 0.0, PC_BR_SHIFT_EV);
-        };
-        auto br_shift = [&]() -> bool {
-            xA = xB; fA = fB; xB = xC; fB = fC; xC = w; fC = fW;
-            return br_loop();
-        };
-        // the CG update after the line search's gradient (PC_G)
-        auto g_step = [&]() -> bool {
-            n_grad++;
-            const double deltaOld = delta;
-            double dl = 0.0;
-#pragma unroll
-            for (int i = 0; i < K; ++i) dl = dl + grad[i] * grad[i];
-            delta = dl;
-            const double beta = delta / deltaOld;       // FLETCHER_REEVES
-            if (iter % K == 0 || beta < 0) {
-#pragma unroll
-                for (int i = 0; i < K; ++i) dir[i] = grad[i];
-            } else {
-#pragma unroll
-                for (int i = 0; i < K; ++i) dir[i] = grad[i] + beta * dir[i];
-            }
-            pc = PC_TOP;
-            return top();
-        };
-        // point[i] += step * searchDirection[i]; r = computeObjectiveGradient(point)
-        auto ls_done = [&]() -> bool {
-            const double step = best_x;
-            memo_obj = best_f;                    // F(point) == Brent's value at `step`
-            bool pfin = true;
-#pragma unroll
-            for (int i = 0; i < K; ++i) {
-                point[i] = point[i] + step * dir[i];
-                pfin = pfin && finite(point[i]);
-            }
-            pc = PC_G;
-            if (!pfin) {                          // the gradient at a non-finite point is NaN: no pass
-#pragma unroll
-                for (int i = 0; i < K; ++i) grad[i] = __builtin_nan("");
-                return g_step();
-            }
-            req = REQ_G;
-            return true;
-        };
-        // one BrentOptimizer iteration: stopping test, then the next point u
-        auto brent_loop = [&]() -> bool {
-            const double m = 0.5 * (a + b);
-            const double tol1 = 1e-15 * dabs(bx) + kBrentAbs;
-            const double tol2 = 2 * tol1;
-            if (dabs(bx - m) <= tol2 - 0.5 * (b - a)) {
-                // return best(best, best(previous, current))
-                double ix = cur_x, iv = cur_f;
-                if (have_prev && prev_f >= cur_f) { ix = prev_x; iv = prev_f; }
-                if (!(best_f >= iv)) { best_x = ix; best_f = iv; }
-                return ls_done();
-            }
-            double p = 0, q = 0, r = 0;
-            if (dabs(be) > tol1) {
-                r = (bx - bw) * (fx - fv);
-                q = (bx - bv) * (fx - fw);
-                p = (bx - bv) * q - (bx - bw) * r;
-                q = 2 * (q - r);
-                if (q > 0) p = -p; else q = -q;
-                r = be;
-                be = bd;
-                if (p > q * (a - bx) && p < q * (b - bx) && dabs(p) < dabs(0.5 * q * r)) {
-                    bd = p / q;
-                    u = bx + bd;
-                    if (u - a < tol2 || b - u < tol2) bd = (bx <= m) ? tol1 : -tol1;
-                } else {
-                    be = (bx < m) ? b - bx : a - bx;
-                    bd = GS * be;
-                }
-            } else {
-                be = (bx < m) ? b - bx : a - bx;
-                bd = GS * be;
-            }
-            if (dabs(bd) < tol1) u = (bd >= 0) ? bx + tol1 : bx - tol1;
-            else u = bx + bd;
-            return eval(u, 0, 0, 0.0, PC_BRENT_FU);
+            ev_bracket = bracket;
+            ev_memo_ok = memo_ok;
+            ev_memo = memo;
+            ev_ret = ret;
+            pc = PC_EVAL;
         };
         for (;;) {
-            bool posted = false;
             switch (pc) {
             case PC_START:
                 // r = computeObjectiveGradient(point)
@@ -512,15 +339,51 @@ struct CGLane {
                 delta = dl;
                 memo_obj = ev_val;                        // F(point) fused into the gradient pass
                 pc = PC_TOP;
-                posted = top();
                 break;
             }
-            case PC_TOP:
-                posted = top();
+            case PC_TOP: {
+                if constexpr (FF) {
+                    // NaN-absorbing state: a non-finite coordinate makes every later evaluation
+                    // NaN (point + alpha * dir is never finite), and with F(point) = NaN the convergence test is
+                    // false, so the reference runs kNanIterEvals evaluations per iteration (one gradient each, at the
+                    // end) until MaxEval. Jump there: the m iterations that still fit complete, the next one stops
+                    // inside with MAX_EVAL at n_eval = kMaxEval (iter <= n_eval / 2, so MaxIter cannot come first).
+                    // Failed fits report NaN coefficients, so the point itself no longer matters.
+                    bool pfin = true;
+#pragma unroll
+                    for (int i = 0; i < K; ++i) pfin = pfin && finite(point[i]);
+                    if (!pfin && __builtin_isnan(memo_obj)) {
+                        const int m = (kMaxEval - (int)n_eval) / kNanIterEvals;
+                        n_grad = (uint16_t)(n_grad + m);
+                        iter = (uint16_t)(iter + m + 1);
+                        n_eval = (uint16_t)kMaxEval;
+                        fail(ARIMA_ST_MAX_EVAL);
+                        return;
+                    }
+                }
+                if (iter + 1 > kMaxIter) { fail(ARIMA_ST_MAX_ITER); return; }
+                iter++;
+                if (n_eval + 1 > kMaxEval) { fail(ARIMA_ST_MAX_EVAL); return; }
+                n_eval++;
+                const double objective = memo_obj;
+                const bool conv = have_prev_obj && value_converged(prev_obj, objective, 1e-7, 1e-7);
+                prev_obj = objective;
+                have_prev_obj = 1;
+                if (conv) { pc = PC_DONE; return; }   // status OK; point / prev_obj are the result
+                // line.search(point, searchDirection)
+                sp_n = sp_next = 0;
+                bcount = 0;
+                xA = 0.0;
+                xB = 1e-8;
+                bool dfin = true;
+#pragma unroll
+                for (int i = 0; i < K; ++i) dfin = dfin && finite(dir[i]);
+                eval(xA, 1, dfin ? 1 : 0, objective, PC_BR_FA);
                 break;
+            }
             case PC_BR_FA:
                 fA = ev_val;
-                posted = eval(xB, 1, 0, 0.0, PC_BR_FB);
+                eval(xB, 1, 0, 0.0, PC_BR_FB);
                 break;
             case PC_BR_FB: {
                 fB = ev_val;
@@ -529,59 +392,122 @@ struct CGLane {
                     t = fA; fA = fB; fB = t;
                 }
                 xC = xB + kGold * (xB - xA);
-                posted = eval(xC, 1, 0, 0.0, PC_BR_FC);
+                eval(xC, 1, 0, 0.0, PC_BR_FC);
                 break;
             }
             case PC_BR_FC:
                 fC = ev_val;
-                posted = br_loop();
+                pc = PC_BR_LOOP;
                 break;
-            case PC_BR_LOOP:
-                posted = br_loop();
+            case PC_BR_LOOP: {
+                if (!(fC > fB)) { pc = PC_BR_END; break; }
+                const double tmp1 = (xB - xA) * (fB - fC);
+                const double tmp2 = (xB - xC) * (fB - fA);
+                const double val = tmp2 - tmp1;
+                const double denom = dabs(val) < kEpsMin ? 2 * kEpsMin : val;
+                w = xB - ((xB - xC) * tmp2 - (xB - xA) * tmp1) / (2 * denom);
+                const double wLim = xB + kGrow * (xC - xB);
+                if ((w - xC) * (xB - w) > 0) {
+                    eval(w, 1, 0, 0.0, PC_BR_A1);
+                } else if ((w - wLim) * (wLim - xC) >= 0) {
+                    w = wLim;
+                    eval(w, 1, 0, 0.0, PC_BR_SHIFT_EV);
+                } else if ((w - wLim) * (xC - w) > 0) {
+                    eval(w, 1, 0, 0.0, PC_BR_C1);
+                } else {
+                    w = xC + kGold * (xC - xB);
+                    eval(w, 1, 0, 0.0, PC_BR_SHIFT_EV);
+                }
                 break;
+            }
             case PC_BR_A1:
                 fW = ev_val;
                 if (fW > fC) {
                     xA = xB; xB = w; fA = fB; fB = fW;
-                    posted = br_end();
+                    pc = PC_BR_END;
                 } else if (fW < fB) {
                     xC = w; fC = fW;
-                    posted = br_end();
+                    pc = PC_BR_END;
                 } else {
                     w = xC + kGold * (xC - xB);
-                    posted = eval(w, 1, 0, 0.0, PC_BR_SHIFT_EV);
+                    eval(w, 1, 0, 0.0, PC_BR_SHIFT_EV);
                 }
                 break;
             case PC_BR_C1:
                 fW = ev_val;
                 if (fW > fC) {
                     xB = xC; xC = w; w = xC + kGold * (xC - xB); fB = fC; fC = fW;
-                    posted = eval(w, 1, 0, 0.0, PC_BR_SHIFT_EV);
+                    eval(w, 1, 0, 0.0, PC_BR_SHIFT_EV);
                 } else {
-                    posted = br_shift();
+                    pc = PC_BR_SHIFT;
                 }
                 break;
             case PC_BR_SHIFT_EV:
                 fW = ev_val;
-                posted = br_shift();
+                pc = PC_BR_SHIFT;
                 break;
             case PC_BR_SHIFT:
-                posted = br_shift();
+                xA = xB; fA = fB; xB = xC; fB = fC; xC = w; fC = fW;
+                pc = PC_BR_LOOP;
                 break;
-            case PC_BR_END:
-                posted = br_end();
+            case PC_BR_END: {
+                // bracket -> Brent (shared storage: read everything needed before writing)
+                double lo = xA, hi = xC;
+                const double mid = xB, fmid = fB;
+                if (lo > hi) { double t = lo; lo = hi; hi = t; }
+                if (lo >= hi || mid < lo || mid > hi) { fail(ARIMA_ST_BAD_INTERVAL); return; }  // SearchInterval
+                if (lo < hi) { a = lo; b = hi; } else { a = hi; b = lo; }
+                bx = bv = bw = mid;
+                bd = be = 0.0;
+                eval(mid, 0, 1, fmid, PC_BRENT_FX);                      // fx = f(mid) (memo: bracket fMid)
                 break;
+            }
             case PC_BRENT_FX:
                 fx = -ev_val;
                 fv = fw = fx;
                 have_prev = 0;
                 cur_x = bx; cur_f = -fx;
                 best_x = cur_x; best_f = cur_f;
-                posted = brent_loop();
+                pc = PC_BRENT_LOOP;
                 break;
-            case PC_BRENT_LOOP:
-                posted = brent_loop();
+            case PC_BRENT_LOOP: {
+                const double m = 0.5 * (a + b);
+                const double tol1 = 1e-15 * dabs(bx) + kBrentAbs;
+                const double tol2 = 2 * tol1;
+                if (dabs(bx - m) <= tol2 - 0.5 * (b - a)) {
+                    // return best(best, best(previous, current))
+                    double ix = cur_x, iv = cur_f;
+                    if (have_prev && prev_f >= cur_f) { ix = prev_x; iv = prev_f; }
+                    if (!(best_f >= iv)) { best_x = ix; best_f = iv; }
+                    pc = PC_LS_DONE;
+                    break;
+                }
+                double p = 0, q = 0, r = 0;
+                if (dabs(be) > tol1) {
+                    r = (bx - bw) * (fx - fv);
+                    q = (bx - bv) * (fx - fw);
+                    p = (bx - bv) * q - (bx - bw) * r;
+                    q = 2 * (q - r);
+                    if (q > 0) p = -p; else q = -q;
+                    r = be;
+                    be = bd;
+                    if (p > q * (a - bx) && p < q * (b - bx) && dabs(p) < dabs(0.5 * q * r)) {
+                        bd = p / q;
+                        u = bx + bd;
+                        if (u - a < tol2 || b - u < tol2) bd = (bx <= m) ? tol1 : -tol1;
+                    } else {
+                        be = (bx < m) ? b - bx : a - bx;
+                        bd = GS * be;
+                    }
+                } else {
+                    be = (bx < m) ? b - bx : a - bx;
+                    bd = GS * be;
+                }
+                if (dabs(bd) < tol1) u = (bd >= 0) ? bx + tol1 : bx - tol1;
+                else u = bx + bd;
+                eval(u, 0, 0, 0.0, PC_BRENT_FU);
                 break;
+            }
             case PC_BRENT_FU: {
                 const double fu = -ev_val;
                 prev_x = cur_x; prev_f = cur_f; have_prev = 1;
@@ -591,10 +517,7 @@ struct CGLane {
                     if (prev_f >= cur_f) { ix = prev_x; iv = prev_f; }
                     if (!(best_f >= iv)) { best_x = ix; best_f = iv; }
                 }
-                if (value_converged(prev_f, cur_f, 1e-8, 1e-8)) {
-                    posted = ls_done();
-                    break;
-                }
+                if (value_converged(prev_f, cur_f, 1e-8, 1e-8)) { pc = PC_LS_DONE; break; }
                 if (fu <= fx) {
                     if (u < bx) b = bx; else a = bx;
                     bv = bw; fv = fw; bw = bx; fw = fx; bx = u; fx = fu;
@@ -603,20 +526,76 @@ struct CGLane {
                     if (fu <= fw || prec_equals(bw, bx)) { bv = bw; fv = fw; bw = u; fw = fu; }
                     else if (fu <= fv || prec_equals(bv, bx) || prec_equals(bv, bw)) { bv = u; fv = fu; }
                 }
-                posted = brent_loop();
+                pc = PC_BRENT_LOOP;
                 break;
             }
-            case PC_LS_DONE:
-                posted = ls_done();
-                break;
-            case PC_G:
-                posted = g_step();
-                break;
-            case PC_DONE:
-            default:                                  // (PC_EVAL is never a resting state: eval runs inline)
+            case PC_LS_DONE: {
+                // point[i] += step * searchDirection[i]; r = computeObjectiveGradient(point)
+                const double step = best_x;
+                memo_obj = best_f;                    // F(point) == Brent's value at `step`
+                bool pfin = true;
+#pragma unroll
+                for (int i = 0; i < K; ++i) {
+                    point[i] = point[i] + step * dir[i];
+                    pfin = pfin && finite(point[i]);
+                }
+                if (!pfin) {                          // the gradient at a non-finite point is NaN: no pass
+#pragma unroll
+                    for (int i = 0; i < K; ++i) grad[i] = __builtin_nan("");
+                    pc = PC_G;
+                    break;
+                }
+                req = REQ_G;
+                pc = PC_G;
                 return;
             }
-            if (posted) return;
+            case PC_G: {
+                n_grad++;
+                const double deltaOld = delta;
+                double dl = 0.0;
+#pragma unroll
+                for (int i = 0; i < K; ++i) dl = dl + grad[i] * grad[i];
+                delta = dl;
+                const double beta = delta / deltaOld;       // FLETCHER_REEVES
+                if (iter % K == 0 || beta < 0) {
+#pragma unroll
+                    for (int i = 0; i < K; ++i) dir[i] = grad[i];
+                } else {
+#pragma unroll
+                    for (int i = 0; i < K; ++i) dir[i] = grad[i] + beta * dir[i];
+                }
+                pc = PC_TOP;
+                break;
+            }
+            case PC_EVAL: {
+                if (ev_bracket) {
+                    if (bcount + 1 > kBracketMax) { fail(ARIMA_ST_BRACKET_MAX_EVAL); return; }
+                    bcount++;
+                }
+                if (n_eval + 1 > kMaxEval) { fail(ARIMA_ST_MAX_EVAL); return; }
+                n_eval++;
+                if (ev_memo_ok) { ev_val = ev_memo; pc = ev_ret; break; }
+                bool fin = true;
+#pragma unroll
+                for (int i = 0; i < K; ++i) fin = fin && finite(point[i] + ev_alpha * dir[i]);
+                if (!fin) { ev_val = __builtin_nan(""); pc = ev_ret; break; }
+                if constexpr (NC > 0) {
+                    const long long ab = dbits(ev_alpha);
+                    bool hit = false;
+#pragma unroll
+                    for (int s = 0; s < NC; ++s)
+                        if (s < sp_n && dbits(sp_alpha[s]) == ab) { ev_val = sp_f[s]; hit = true; }
+                    if (hit) { spec_hits++; pc = ev_ret; break; }
+                }
+                rq_nspec = (uint8_t)predict(ev_ret);
+                req = REQ_F;
+                pc = (uint8_t)ev_ret;                  // resume point once the response arrives
+                return;
+            }
+            case PC_DONE:
+            default:
+                return;
+            }
         }
     }
 };

@@ -66,7 +66,8 @@ class FitStats(ctypes.Structure):
                 ("express_pit_passes", ctypes.c_int64), ("express_pit_sweeps", ctypes.c_int64),
                 ("express_pit_g_passes", ctypes.c_int64), ("wave_chains", ctypes.c_int64),
                 ("low_util_passes", ctypes.c_int64), ("diag_step_cycles", ctypes.c_int64),
-                ("diag_refill_cycles", ctypes.c_int64)]
+                ("diag_refill_cycles", ctypes.c_int64), ("merge_series", ctypes.c_int64),
+                ("merge_waves", ctypes.c_int64)]
 
     def as_dict(self):
         d = {name: getattr(self, name) for name, _ in self._fields_}

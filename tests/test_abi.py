@@ -66,3 +66,19 @@ def test_product_path_fails_loudly_without_gpu():
     from sparkts_amd.models import ARIMA
     with pytest.raises(L.EngineError):
         ARIMA.fit_model(1, 0, 1, [1.0, 2.0, 3.0, 5.0, 4.0, 6.0, 5.0, 7.0])
+
+
+def test_stats_struct_matches_binding():
+    # arima_fit_stats (include/sparkts_arima.h) and the ctypes mirror (sparkts_amd._lib.FitStats): same fields, same
+    # order, same types -- arima_get_last_stats writes the C layout into the Python structure
+    import sparkts_amd._lib as L
+    txt = open(HEADER).read()
+    body = txt[txt.index("typedef struct arima_fit_stats {"):txt.index("} arima_fit_stats;")]
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    fields = re.findall(r"\b(int64_t|double|int32_t)\s+(\w+)\s*(?:\[(\d+)\])?\s*;", body)
+    ctypes_of = {"int64_t": ctypes.c_int64, "double": ctypes.c_double, "int32_t": ctypes.c_int32}
+    want = [(n, ctypes_of[t] * int(k) if k else ctypes_of[t]) for t, n, k in fields]
+    got = list(L.FitStats._fields_)
+    assert [n for n, _ in want] == [n for n, _ in got]
+    for (n, a), (_, b) in zip(want, got):
+        assert ctypes.sizeof(a) == ctypes.sizeof(b) and getattr(a, "_type_", a) == getattr(b, "_type_", b), n

@@ -483,6 +483,52 @@ def test_pipelined_device_fits_match_serial(engine, pipeline):
             assert _same(x, y), (pipeline, orders[i])
 
 
+@pytest.mark.parametrize("xblocks", [-1, 0])
+def test_drain_merge_is_transparent(engine, xblocks):
+    # k_cg_fit's drain merge (option merge_live): once the work counter has run out, a wave with few live slots
+    # hands them to the merge pool and leaves, and waves still running take them into free slots. Only where a
+    # series is fitted changes: outputs bit-identical with the merge off, at the default and at 64 (every drained
+    # wave offers its slots: the protocol's worst case), with and without express waves; every series written,
+    # no watchdog fault; a subsample against the oracle.
+    import torch
+    N, T = 1 << 18, 1024
+    s = _device_sample(engine, N, T, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 4242)
+    outs = {}
+    dflt = engine.get_option("merge_live")
+    engine.set_option("express_blocks", xblocks)
+    try:
+        for ml in (0, 16, 64):
+            engine.set_option("merge_live", ml)
+            r = [torch.empty((N, 5), dtype=torch.float64, device=s.device),
+                 torch.empty(N, dtype=torch.float64, device=s.device)] + \
+                [torch.empty(N, dtype=torch.int32, device=s.device) for _ in range(3)] + \
+                [torch.empty(N, dtype=torch.uint8, device=s.device)]
+            engine.fit_batch_device(s.data_ptr(), N, T, T, 2, 1, 2, True, *[t.data_ptr() for t in r])
+            st = engine.stats()
+            outs[ml] = ([t.cpu().numpy() for t in r], st)
+    finally:
+        engine.set_option("merge_live", dflt)
+        engine.set_option("express_blocks", -1)
+    base, st0 = outs[0]
+    assert st0["merge_series"] == 0 and st0["merge_waves"] == 0, st0
+    for ml in (16, 64):
+        o, st = outs[ml]
+        for x, y in zip(base, o):
+            assert _same(x, y), ml
+        assert st["series_done"] == N and st["fault"] == 0, st
+        assert st["merge_waves"] > 0 and st["merge_series"] > 0, st
+        assert st["n_eval"] == st0["n_eval"] and st["n_grad"] == st0["n_grad"], (st, st0)
+    rows = np.arange(0, N, N // 256)
+    sh = s[torch.as_tensor(rows, device=s.device)].cpu().numpy()
+    st_o, coef, ll, cnt = O.fit_batch(sh, 2, 1, 2, 1)
+    o = outs[64][0]
+    exp = dict(status=st_o, coef=coef, ll=ll, n_eval=cnt[:, 0], n_grad=cnt[:, 1],
+               flags=np.array([O.model_flags(coef[i], 2, 2, 1) if st_o[i] == 0 else 0 for i in range(len(rows))]))
+    res = dict(coef=o[0][rows], ll=o[1][rows], status=o[2][rows], n_eval=o[3][rows], n_grad=o[4][rows],
+               flags=o[5][rows])
+    check_fit(res, exp, f"merge64 xblocks={xblocks}")
+
+
 def test_c4_T4096_vs_oracle(engine):
     # C4 at its own length (BASELINE.json configs[3]): ARIMA(5,1,5)+c, T = 4096, 48 device-generated series checked
     # against the oracle -- status (MaxEval / bracket failures included), n_eval, n_grad, coefficients, LL, flags
