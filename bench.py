@@ -587,6 +587,8 @@ def run_c5(args, eng, series, N, T, total_series, world, rank, dev, barrier, dis
                        "series_per_gpu": N, "series_total": total_series, "fits_per_series": 216,
                        "fits_per_sec": total_series * 216 * args.steps / elapsed,
                        "search_lanes": eng.get_option("search_lanes"),
+                       "search_express_cus": eng.get_option("search_express_blocks"),
+                       "merge_live": eng.get_option("merge_live"),
                        "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                        "found_fraction": found, "selected_orders_top":
                            dict(sorted(sel.items(), key=lambda kv: -kv[1])[:6]),

@@ -130,7 +130,10 @@ int         arima_synchronize(arima_handle *h);
  * (differenced workspace of one slice of a large device fit), "express_ring" (express hand-offs per launch),
  * "row_pad" (doubles added to the stride of the differenced-row workspaces, whole 128-B lines, default 0),
  * "merge_live" (k_cg_fit drain merge: after the batch's work counter ran out, a wave with at most this many live
- * series hands them to waves still running and exits, 0..64, 0 = off; results never depend on it). */
+ * series hands them to waves still running and exits, 0..64, 0 = off; results never depend on it),
+ * "search_express_blocks" (express CUs of each concurrent order-search fit, default 0; -1 = as "express_blocks"),
+ * "donate_evals" / "donate_evals_drained" (evaluations before a series may move to an express wave, before / after
+ * the batch's work counter ran out; 0 = the kernel's 256 / 32). */
 int         arima_set_option(arima_handle *h, const char *name, int64_t value);
 /* Current value of a tuning knob (the names arima_set_option takes); ARIMA_E_INVALID_ARG for an unknown name. */
 int         arima_get_option(const arima_handle *h, const char *name, int64_t *value);

@@ -290,8 +290,9 @@ constexpr int kExpressTagWord = kExpressEntryBytes / 8 - 1;
 // ring entries this launch may fill: ctl[19] when the host set it (option "express_ring", tests reach the cap with a
 // small ring), else the whole ring. Tickets beyond it are never filled (their groups retire); their series stay on
 // the bulk path, so reaching the cap changes where a series is fitted, never its result.
-// With the drain merge on (ctl[44] > 0) the ring's upper half is the merge pool, so hand-offs stop at its lower half.
-constexpr int kMergeCap = kExpressRing / 2;  // merge pool entries per launch (never reused within it)
+// With the drain merge on (ctl[44] > 0) the ring's upper three quarters are the merge pool, so hand-offs stop at the
+// lower quarter (8 192).
+constexpr int kMergeCap = kExpressRing / 4 * 3;   // merge pool entries per launch (never reused within it)
 __device__ __forceinline__ unsigned long long express_ring_entries(const unsigned long long *ctl) {
     const unsigned long long r = ctl[19];
     const unsigned long long cap = ctl[44] ? (unsigned long long)(kExpressRing - kMergeCap) : (unsigned long long)kExpressRing;
@@ -702,8 +703,8 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     // Drain merge (round 4; ctl[44] = merge_live > 0, set by the host): once the batch's work counter has run out,
-    // a wave whose live slots dropped to merge_live or fewer hands them to the merge pool (the upper half of the
-    // express ring) and leaves; waves still running take pool entries into their free slots (up to 64 live). Few
+    // a wave whose live slots dropped to merge_live or fewer hands them to the merge pool (the upper three quarters
+    // of the express ring) and leaves; waves still running take pool entries into their free slots (up to 64 live). Few
     // waves then run nearly full passes instead of many nearly empty ones, and a leaving wave's SIMD (its whole
     // workgroup, once all four left) goes to the next fit sharing the GPU. ctl[40] = active waves (bits 0-23) |
     // entries reserved (bits 24-63), ctl[41] = entries claimed, ctl[42] = waves that handed over, ctl[43] = claims.
@@ -715,6 +716,9 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
     unsigned *mready = xready + (kExpressRing - kMergeCap);
     unsigned long long merge_head = 0;     // entries claimed, as last seen (a lower bound)
     if (merge_live > 0 && lane == 0) add_agent(&ctl[40], 1ull);
+    // donation thresholds: ctl[45] / ctl[46] when the host set them (options "donate_evals" / "donate_evals_drained")
+    const int don_evals = ctl[45] ? (int)ctl[45] : kDonateEvals;
+    const int don_drained = ctl[46] ? (int)ctl[46] : kDonateEvalsDrained;
     FitSlot<K> *ws = slots[wave];
     const unsigned long long xring = express_ring_entries(ctl);
     unsigned long long lane_f = 0, lane_g = 0, wave_f = 0, wave_g = 0, wave_m = 0, evals = 0, grads = 0, hits = 0,
@@ -1158,7 +1162,7 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
             fault = __shfl(fault, 0);
             // no donation once a fault is recorded (a retired ticket holder would never write it back)
             if (wants > filled && filled < xring && fault == 0) {
-                const int donate_min = __any(drained) ? kDonateEvalsDrained : kDonateEvals;
+                const int donate_min = __any(drained) ? don_drained : don_evals;
                 unsigned long long key = 0;
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) {

@@ -133,7 +133,13 @@ struct arima_handle {
     int grid_blocks_override = 0;
     int express_blocks = -1;       // k_cg_fit express workgroups (-1: num_cus / 16)
     int express_ring = 0;          // express hand-offs per launch (0: the whole ring, sts::kExpressRingEntries)
-    int merge_live = STS_MERGE_LIVE_DEFAULT;   // k_cg_fit drain merge: hand over at <= this many live slots (0: off)
+    int merge_live = STS_MERGE_LIVE_DEFAULT;
+    // express CUs of the order search's concurrent fits (-1: as "express_blocks"). 0 by default: with 16 lanes in
+    // flight each fit's express workgroups held whole CUs for the fit's duration, mostly waiting (C5 262 144:
+    // 14 728 series/s with them, 16 659 without; profiles/r04/g_merge)
+    int search_express_blocks = 0;
+    int donate_evals = 0;          // k_cg_fit: evaluations before a slot may go to an express wave (0: kernel default)
+    int donate_evals_drained = 0;  // ... once the batch's work counter has run out (0: kernel default)   // k_cg_fit drain merge: hand over at <= this many live slots (0: off)
     int hr_grid = 0;               // k_hr_init: 0 = a lane per series; > 0 = that many single-wave workgroups
     int row_pad = 0;               // doubles (multiple of 16) added to the differenced rows' stride
     int fit_kernel = 0;            // 0: k_cg_fit (LDS slots, 1 wave/SIMD); 2: rounds of streaming passes + k_cg_fit
@@ -510,6 +516,15 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
         h->express_ring = (int)std::min<int64_t>(sts::kExpressRingEntries, std::max<int64_t>(0, value));
         return ARIMA_OK;
     }
+    if (!strcmp(name, "search_express_blocks")) {
+        h->search_express_blocks = (int)std::max<int64_t>(-1, value);
+        return ARIMA_OK;
+    }
+    if (!strcmp(name, "donate_evals")) { h->donate_evals = (int)std::max<int64_t>(0, value); return ARIMA_OK; }
+    if (!strcmp(name, "donate_evals_drained")) {
+        h->donate_evals_drained = (int)std::max<int64_t>(0, value);
+        return ARIMA_OK;
+    }
     if (!strcmp(name, "merge_live")) { h->merge_live = (int)std::min<int64_t>(64, std::max<int64_t>(0, value)); return ARIMA_OK; }
     if (!strcmp(name, "express_blocks")) { h->express_blocks = (int)std::max<int64_t>(-1, value); return ARIMA_OK; }
     if (!strcmp(name, "grid_blocks")) { h->grid_blocks_override = (int)std::max<int64_t>(0, value); return ARIMA_OK; }
@@ -541,7 +556,9 @@ int arima_get_option(const arima_handle *hc, const char *name, int64_t *value) {
         {"fit_kernel", h->fit_kernel}, {"hr_grid", h->hr_grid}, {"row_pad", h->row_pad}, {"rounds_max", h->rounds_max},
         {"rounds_tail", h->rounds_tail}, {"rounds_pass_waves", h->rounds_pass_waves},
         {"rounds_tail_express", h->rounds_tail_express}, {"rounds_tail_cus", h->rounds_tail_cus},
-        {"rounds_tail_xcus", h->rounds_tail_xcus}, {"merge_live", h->merge_live}};
+        {"rounds_tail_xcus", h->rounds_tail_xcus}, {"merge_live", h->merge_live},
+        {"search_express_blocks", h->search_express_blocks}, {"donate_evals", h->donate_evals},
+        {"donate_evals_drained", h->donate_evals_drained}};
     for (const auto &o : opts)
         if (!strcmp(name, o.n)) {
             *value = o.v;
@@ -598,7 +615,8 @@ static int ensure_rounds_ws(arima_handle *h, FitWs &ws, int64_t N, int k) {
 static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn, int n, int64_t N, int32_t p,
                        int32_t q, int32_t I, int32_t method, const double *d_user_init, double *d_coef, double *d_ll,
                        int32_t *d_status, int32_t *d_neval, int32_t *d_ngrad, uint8_t *d_flags, hipStream_t s,
-                       hipEvent_t ev_mid, int64_t *grid_out, int64_t *express_out, bool shared_gpu = false) {
+                       hipEvent_t ev_mid, int64_t *grid_out, int64_t *express_out, bool shared_gpu = false,
+                       int express_cus = -2) {
     const int k = I + p + q;
     *grid_out = 0;
     *express_out = 0;
@@ -609,6 +627,11 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
         HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)(ws.ctl.as<unsigned long long>() + 19), h->express_ring, 1, s));
     if (h->merge_live > 0)                                     // ctl[44]: k_cg_fit's drain merge threshold
         HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)(ws.ctl.as<unsigned long long>() + 44), h->merge_live, 1, s));
+    if (h->donate_evals > 0)                                   // ctl[45] / ctl[46]: express donation thresholds
+        HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)(ws.ctl.as<unsigned long long>() + 45), h->donate_evals, 1, s));
+    if (h->donate_evals_drained > 0)
+        HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)(ws.ctl.as<unsigned long long>() + 46), h->donate_evals_drained, 1,
+                                    s));
     if (p > 0 && q == 0) {                                     // AR-only shortcut, method never checked
         if (ev_mid) HIPCHK(h, hipEventRecord(ev_mid, s));
         RCCHK(h, sts::launch_ar_fit(y, ldn, n, N, p, I, d_coef, d_ll, d_status, d_neval, d_ngrad, d_flags, s),
@@ -639,7 +662,9 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
     // workgroups (k_cg_fit's long-series path); fewer bulk blocks when the batch cannot fill them
     // (express_blocks and grid_blocks count CUs' worth of workgroups: x kFitBlocksPerCU single-wave workgroups)
     const int cus = std::max(1, h->num_cus);
-    int xcus = h->express_blocks >= 0 ? h->express_blocks : std::max(1, cus / 16);
+    // (express_cus: the caller's count, -2 = the "express_blocks" option; the order search passes its own)
+    const int xopt = express_cus >= -1 ? express_cus : h->express_blocks;
+    int xcus = xopt >= 0 ? xopt : std::max(1, cus / 16);
     if (xcus >= cus) xcus = cus - 1;
     int bcus = h->grid_blocks_override;
     if (bcus <= 0) bcus = std::max(1, cus - xcus);
@@ -651,7 +676,7 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
     const int per_block = std::max(1, sts::cg_fit_series_per_block(p, q, I, variant));
     const int64_t need = (N + per_block - 1) / per_block;
     if (blocks > need) blocks = (int)need;
-    if (xblocks > 0 || h->merge_live > 0) {                   // the merge pool is the ring's upper half
+    if (xblocks > 0 || h->merge_live > 0) {                   // the merge pool: the ring's upper 3/4
         RCCHK(h, ws.xring.ensure(sts::kExpressRingBytes), "workspace");
         RCCHK(h, ws.xready.ensure(sts::kExpressReadyBytes), "workspace");
         HIPCHK(h, hipMemsetAsync(ws.xready.ptr, 0, sts::kExpressReadyBytes, s));
@@ -1429,7 +1454,7 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
                 RCCHK(h, fit_kernels(h, ln.ws, dbuf.as<double>(), ldn, n, N, p, q, I, method, nullptr,
                                      ln.coef.as<double>(), ln.ll.as<double>(), ln.status.as<int32_t>(),
                                      ln.neval.as<int32_t>(), ln.ngrad.as<int32_t>(), ln.flags.as<uint8_t>(), ln.stream,
-                                     nullptr, &gridb, &xb, L > 1), "fit");
+                                     nullptr, &gridb, &xb, L > 1, L > 1 ? h->search_express_blocks : -2), "fit");
                 hipLaunchKernelGGL(k_search_acc, dim3(1), dim3(64), 0, ln.stream, ln.ws.ctl.as<unsigned long long>(),
                                    ln.acc.as<unsigned long long>(), N, n, p, q, I,
                                    (p > 0 && q == 0) || method != ARIMA_METHOD_CSS_CGD || I + p + q == 0 ? 0 : 1);
