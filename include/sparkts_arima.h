@@ -126,7 +126,8 @@ int         arima_synchronize(arima_handle *h);
  * "grid_blocks", "search_lanes" (in-kernel scheduler and order-search concurrency), "fit_kernel" (0: k_cg_fit with
  * LDS-resident optimizer slots; 2: rounds of streaming passes, then k_cg_fit on the last series; 3: k_cg_fit_r, two
  * waves per SIMD with one optimizer slot per lane in registers, rows up to cg_fit_reg_max_n), "rounds_max",
- * "rounds_tail", "rounds_pass_waves" (fit_kernel 2), "hr_grid" (k_hr_init grid), "fit_slice_bytes"
+ * "rounds_tail", "rounds_pass_waves" (fit_kernel 2), "hr_grid" (k_hr_init grid: 0 = a lane per series, > 0 = that
+ * many single-wave workgroups, -1 = 1024 for pipelined fits else 0), "fit_slice_bytes"
  * (differenced workspace of one slice of a large device fit), "express_ring" (express hand-offs per launch),
  * "row_pad" (doubles added to the stride of the differenced-row workspaces, whole 128-B lines, default 0),
  * "merge_live" (k_cg_fit drain merge: after the batch's work counter ran out, a wave with at most this many live

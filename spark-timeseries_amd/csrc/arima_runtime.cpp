@@ -140,7 +140,10 @@ struct arima_handle {
     int search_express_blocks = 0;
     int donate_evals = 0;          // k_cg_fit: evaluations before a slot may go to an express wave (0: kernel default)
     int donate_evals_drained = 0;  // ... once the batch's work counter has run out (0: kernel default)   // k_cg_fit drain merge: hand over at <= this many live slots (0: off)
-    int hr_grid = 0;               // k_hr_init: 0 = a lane per series; > 0 = that many single-wave workgroups
+    // k_hr_init: 0 = a lane per series; > 0 = that many single-wave workgroups (grid-stride); -1 (default) = 1 024
+    // for pipelined device fits (fit_pipeline > 1: C2 9.47-9.55 -> 9.68-9.75 M series/s, profiles/r04/m_hrgrid),
+    // else 0 (alone it is 25.2 vs 26.9 ms at C2)
+    int hr_grid = -1;
     int row_pad = 0;               // doubles (multiple of 16) added to the differenced rows' stride
     int fit_kernel = 0;            // 0: k_cg_fit (LDS slots, 1 wave/SIMD); 2: rounds of streaming passes + k_cg_fit
     int rounds_max = 96;           // rounds enqueued per fit (fit_kernel 2)
@@ -511,7 +514,7 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
         h->row_pad = (int)round_up(std::min<int64_t>(4096, std::max<int64_t>(0, value)), 16);
         return ARIMA_OK;
     }
-    if (!strcmp(name, "hr_grid")) { h->hr_grid = (int)std::min<int64_t>(1 << 20, std::max<int64_t>(0, value)); return ARIMA_OK; }
+    if (!strcmp(name, "hr_grid")) { h->hr_grid = (int)std::min<int64_t>(1 << 20, std::max<int64_t>(-1, value)); return ARIMA_OK; }
     if (!strcmp(name, "express_ring")) {
         h->express_ring = (int)std::min<int64_t>(sts::kExpressRingEntries, std::max<int64_t>(0, value));
         return ARIMA_OK;
@@ -616,7 +619,7 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
                        int32_t q, int32_t I, int32_t method, const double *d_user_init, double *d_coef, double *d_ll,
                        int32_t *d_status, int32_t *d_neval, int32_t *d_ngrad, uint8_t *d_flags, hipStream_t s,
                        hipEvent_t ev_mid, int64_t *grid_out, int64_t *express_out, bool shared_gpu = false,
-                       int express_cus = -2) {
+                       int express_cus = -2, bool search = false) {
     const int k = I + p + q;
     *grid_out = 0;
     *express_out = 0;
@@ -644,7 +647,7 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
         RCCHK(h, ws.init.ensure((size_t)N * std::max(k, 1) * sizeof(double)), "workspace");
         RCCHK(h, ws.hr_status.ensure((size_t)N * sizeof(int32_t)), "workspace");
         RCCHK(h, sts::launch_hr_init(y, ldn, n, N, p, q, I, ws.init.as<double>(), ws.hr_status.as<int32_t>(), s,
-                                     h->hr_grid),
+                                     h->hr_grid >= 0 ? h->hr_grid : (shared_gpu && !search ? 1024 : 0)),
               "hr_init");
         init = ws.init.as<double>();
         init_status = ws.hr_status.as<int32_t>();
@@ -1238,7 +1241,7 @@ int arima_hannan_rissanen_batch(arima_handle *h, const double *diffed, int64_t N
     RCCHK(h, h->h_coef.ensure((size_t)N * std::max(k, 1) * sizeof(double)), "staging");
     RCCHK(h, h->h_status.ensure((size_t)N * sizeof(int32_t)), "staging");
     RCCHK(h, sts::launch_hr_init(h->diff.as<double>(), ld, n, N, p, q, I, h->h_coef.as<double>(),
-                                 h->h_status.as<int32_t>(), s, h->hr_grid), "hr_init");
+                                 h->h_status.as<int32_t>(), s, std::max(h->hr_grid, 0)), "hr_init");
     if (k > 0) HIPCHK(h, hipMemcpyAsync(init_out, h->h_coef.ptr, (size_t)N * k * sizeof(double), hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipMemcpyAsync(status_out, h->h_status.ptr, (size_t)N * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     HIPCHK(h, end_call(h, s));
@@ -1454,7 +1457,7 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
                 RCCHK(h, fit_kernels(h, ln.ws, dbuf.as<double>(), ldn, n, N, p, q, I, method, nullptr,
                                      ln.coef.as<double>(), ln.ll.as<double>(), ln.status.as<int32_t>(),
                                      ln.neval.as<int32_t>(), ln.ngrad.as<int32_t>(), ln.flags.as<uint8_t>(), ln.stream,
-                                     nullptr, &gridb, &xb, L > 1, L > 1 ? h->search_express_blocks : -2), "fit");
+                                     nullptr, &gridb, &xb, L > 1, L > 1 ? h->search_express_blocks : -2, true), "fit");
                 hipLaunchKernelGGL(k_search_acc, dim3(1), dim3(64), 0, ln.stream, ln.ws.ctl.as<unsigned long long>(),
                                    ln.acc.as<unsigned long long>(), N, n, p, q, I,
                                    (p > 0 && q == 0) || method != ARIMA_METHOD_CSS_CGD || I + p + q == 0 ? 0 : 1);
