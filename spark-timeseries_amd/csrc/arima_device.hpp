@@ -159,11 +159,13 @@ __device__ __forceinline__ void stream_elems(const double *__restrict__ row, int
 // [e_{t-1}, e_{t-2}, e_{t-2}, ...] (a smear for q >= 3, exactly what the reference computes).
 // ------------------------------------------------------------------------------------------------------
 #ifndef STS_PREFETCH_F
-#define STS_PREFETCH_F 4
+#define STS_PREFETCH_F 3
 #endif
 #ifndef STS_PREFETCH_G
-#define STS_PREFETCH_G 2
+#define STS_PREFETCH_G 1
 #endif
+// (round 4: 4 / 2 -> 3 / 1 on one box: pipelined C2 9.47-9.59 -> 10.47-10.58 M series/s, isolated launch 138.5 ->
+// 128.6 ms, profiles/r04/p_pf; registers and scratch of k_cg_fit unchanged -- the F pass's inner loop schedules better)
 constexpr int kPrefetchF = STS_PREFETCH_F;   // chunks in flight per lane in objective passes
 constexpr int kPrefetchG = STS_PREFETCH_G;   // ... in gradient passes (5x the VALU work per byte)
 
