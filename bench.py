@@ -249,7 +249,9 @@ def main():
     ap.add_argument("--e2e", type=int, default=1, choices=[0, 1])
     ap.add_argument("--fit-kernel", type=int, default=-1, help="0: k_cg_fit (LDS slots), 2: rounds of streaming passes; -1: default")
     ap.add_argument("--device", type=int, default=None, help="GPU of every rank (default: LOCAL_RANK's)")
-    ap.add_argument("--search-lanes", type=int, default=0, help="c5: concurrent search lanes (0: 16)")
+    ap.add_argument("--search-lanes", type=int, default=0,
+                    help="c5: concurrent search lanes (0: 12; 8 / 10 / 12 / 16 / 24 lanes: 18.1 / 20.3 / 21.3 / 19.5 / "
+                         "18.2 k series/s at 262 144, profiles/r04/w_lanes, v_cfg)")
     ap.add_argument("--dry-run", action="store_true")
     args = ap.parse_args()
     if args.device is not None:
@@ -321,7 +323,7 @@ def main():
     if args.grid_blocks:
         eng.set_option("grid_blocks", args.grid_blocks)
     if args.config == "c5":
-        eng.set_option("search_lanes", args.search_lanes or 16)
+        eng.set_option("search_lanes", args.search_lanes or 12)
 
     series = torch.empty((N, T), dtype=torch.float64, device=dev)
     eng.sample_device(series.data_ptr(), N, T, T, p, d, q, I, base, jitter, SEED, first)
