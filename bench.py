@@ -35,8 +35,8 @@ import time
 # GPU_MAX_HW_QUEUES hardware queues (default 4), and kernels of streams that share a queue run one after the other:
 # 6 contexts + the handle's stream need 8 queues to overlap (C2: 8.65 M series/s with 4 queues and 3 contexts,
 # 9.5-9.7 with 8-16 queues and 6-8 contexts; C5's 8 search lanes: 4638 -> 5497 series/s; profiles/r03/j_hwq/{a,b}).
-# The C5 order search runs 16 search lanes, which need 16 + 2 queues (8 lanes on 8 queues: 10 654 series/s at
-# 262 144 x 1024; 16 lanes on 24 queues: 12 976; 16 lanes on 16 queues: no gain over 8, profiles/r03/q_lanes).
+# The C5 order search runs 12 search lanes (round 4; 16 in round 3), which need lanes + 2 queues (round 3: 8 lanes on
+# 8 queues 10 654 series/s at 262 144 x 1024, 16 lanes on 24 queues 12 976, profiles/r03/q_lanes); 24 queues kept.
 # Set before anything initialises HIP (the GPU boxes export 4); a larger setting in the environment is kept.
 _C5 = any(a == "--config=c5" for a in sys.argv) or any(
     a == "--config" and i + 1 < len(sys.argv) and sys.argv[i + 1] == "c5" for i, a in enumerate(sys.argv))
