@@ -235,8 +235,8 @@ def end_to_end(eng, series, p, d, q, I):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=None, help="timed steps (default: 20 for c2/c3, 5 for c4, 2 for c5)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed warmup steps (default: 3; 1 for c5)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--series", type=int, default=1 << 20, help="series per GPU (weak scaling)")
     ap.add_argument("--total-series", type=int, default=0, help="fixed total series over all GPUs (strong scaling)")
@@ -279,6 +279,10 @@ def main():
         dist.init_process_group("gloo")
 
     p, d, q, I, T, base, jitter = CONFIGS[args.config]
+    if args.steps is None:                  # enough steps that the pipeline's fill is amortised (C2: 3 steps read
+        args.steps = {"c4": 5, "c5": 2}.get(args.config, 20)   # 9.35 M series/s, 20 steps 11.0, profiles/r04/zz_check)
+    if args.warmup is None:
+        args.warmup = 1 if args.config == "c5" else 3
     if args.pipeline <= 0:
         args.pipeline = 4 if args.config == "c4" else 6
     if args.config == "c5" and not args.total_series:
