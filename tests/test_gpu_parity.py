@@ -597,6 +597,44 @@ def test_order_search_lane_count_is_transparent(engine):
     assert np.all(res[8][0][:, 0] >= 0)
 
 
+def test_order_search_express_and_hr_grid_are_transparent(engine):
+    # round-4 defaults that only move work: the search's concurrent fits without express waves (search_express_blocks
+    # 0) vs with them (-1: as a single fit), and the HR init as capped grids of single-wave workgroups (hr_grid) vs a
+    # lane per series -- selections, approxAIC and coefficients bit-identical
+    s = _device_sample(engine, 4096, 512, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 7).cpu().numpy()
+    res = {}
+    try:
+        for sx, hg in ((0, -1), (-1, -1), (0, 256), (0, 0)):
+            engine.set_option("search_express_blocks", sx)
+            engine.set_option("hr_grid", hg)
+            res[(sx, hg)] = engine.order_search(s, 3, 2, 3, 2)
+    finally:
+        engine.set_option("search_express_blocks", 0)
+        engine.set_option("hr_grid", -1)
+    base = res[(0, -1)]
+    for key, r in res.items():
+        for x, y in zip(base, r):
+            assert _same(np.asarray(x), np.asarray(y)), key
+    assert np.all(base[0][:, 0] >= 0)
+
+
+@pytest.mark.parametrize("hr_grid", [0, 256, 1024])
+def test_hr_grid_is_transparent(engine, hr_grid):
+    # k_hr_init with a lane per series (0) or a capped grid of single-wave workgroups striding over the series: the
+    # same Householder per lane, so the inits -- and the fits from them -- are bit-identical to the oracle either way
+    N, T = 2048, 1024
+    s = _device_sample(engine, N, T, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 31).cpu().numpy()
+    engine.set_option("hr_grid", hr_grid)
+    try:
+        res = engine.fit_batch(s, 2, 1, 2, True)
+    finally:
+        engine.set_option("hr_grid", -1)
+    st, coef, ll, cnt = O.fit_batch(s, 2, 1, 2, 1)
+    exp = dict(status=st, coef=coef, ll=ll, n_eval=cnt[:, 0], n_grad=cnt[:, 1],
+               flags=np.array([O.model_flags(coef[i], 2, 2, 1) if st[i] == 0 else 0 for i in range(N)]))
+    check_fit(res, exp, f"hr_grid={hr_grid}")
+
+
 def test_wire_format_partition_fit_matches_oracle(engine):
     # records in the JVM <-> Python wire format (PythonConnector.scala:59-88) through fit_arima_records: the
     # coefficients that come back, decoded, equal the oracle's (NaN for failed fits); two series lengths in one
