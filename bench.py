@@ -19,6 +19,10 @@ collective; gloo carries only the timing barrier and the max-over-ranks reductio
   --e2e 0|1         also time one arima_fit_batch call from pageable host memory (default 1)
   --config c5       BASELINE.json configs[4]: a step = the full (d <= 2, p <= 5, q <= 5, +-c) min-approxAIC order search
                     over this rank's shard (strong scaling over --total-series, default 1M); unit series searched/sec
+  --config c1       BASELINE.json configs[0]: ARIMA(1,0,1)+c on 10 000 series x 500 pts (the reference's CPU config)
+  --config c4       BASELINE.json configs[3]: ARIMA(5,1,5)+c on 1M series x 4096 pts (the long-series path)
+  --default-leg 0|1 c2, one GPU: also time the drop-in exactly as a caller gets it -- arima_fit_batch_device with the
+                    ABI's default options, in a child process that keeps the box's GPU_MAX_HW_QUEUES (default 1)
   --device D        bind every rank to GPU D (also SPARKTS_DEVICE) instead of LOCAL_RANK's: several ranks on one GPU
   --dry-run         no GPU: ranks compute their shards and report (tests/test_multirank.py)
 Prints ONE JSON line on rank 0.
@@ -41,7 +45,8 @@ import time
 _C5 = any(a == "--config=c5" for a in sys.argv) or any(
     a == "--config" and i + 1 < len(sys.argv) and sys.argv[i + 1] == "c5" for i, a in enumerate(sys.argv))
 _QUEUES = 24 if _C5 else 8
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or "4") < _QUEUES:
+_BOX_QUEUES = os.environ.get("GPU_MAX_HW_QUEUES")            # the box's own setting (the default-config leg keeps it)
+if not os.environ.get("SPARKTS_BENCH_DEFAULT_LEG") and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or "4") < _QUEUES:
     os.environ["GPU_MAX_HW_QUEUES"] = str(_QUEUES)
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -52,7 +57,13 @@ CONFIGS = {
     "c5": (2, 1, 2, 1, 1024, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05),
     "c2": (2, 1, 2, 1, 1024, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05),
     "c1": (1, 0, 1, 1, 500, [3.5, 0.3, 0.7], 0.05),
-    "c4": (5, 1, 5, 1, 4096, [0.1, 0.4, -0.2, 0.1, 0.05, -0.05, 0.3, 0.2, -0.1, 0.05, 0.05], 0.02),
+    "c4": (5, 1, 5, 1, 4096, [0.1, 0.4, -0.2, 0.1, 0.05, -0.05, 0.3, 0.2, -0.1, 0.05, 0.05], 0.05),
+}
+DEFAULT_SERIES = {"c1": 10000}                 # configs[0]: 10k series; every other config 1M per GPU
+METRICS = {
+    "c2": "series fitted/sec, ARIMA(2,1,2) CSS-CGD, 1M x 1024 pts",
+    "c1": "series fitted/sec, ARIMA(1,0,1) CSS-CGD, 10k x 500 pts (BASELINE.json configs[0])",
+    "c4": "series fitted/sec, ARIMA(5,1,5)+c CSS-CGD, 1M x 4096 pts (BASELINE.json configs[3])",
 }
 FP64_PEAK_TFLOPS = 78.6    # MI355X fp64 vector peak (spec)
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md)
@@ -103,11 +114,6 @@ def physical_cores():
         return len(pairs) or None
     except OSError:
         return None
-
-
-def eng_fit_kernel(eng):
-    """The fit kernel variant the engine runs (option fit_kernel)."""
-    return eng.get_option("fit_kernel")
 
 
 def log(*a):
@@ -182,6 +188,90 @@ def cpu_baseline(series_host, p, d, q, I, smear, target_s):
                       f"not the spark-ts JVM"}
 
 
+def oracle_rows(series_host, p, d, q, I, smear, budget_s):
+    """The CPU restatement's fits of the first rows of this rank's shard (the parity check of ranks that do not time
+    a CPU baseline): chunks of rows until every row is fitted or about budget_s seconds have passed."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    affinity = len(os.sched_getaffinity(0))
+    O.set_threads(max(1, min(int(os.environ.get("OMP_NUM_THREADS", "0") or "0") or affinity, affinity, 64)))
+    parts = []
+    t0 = time.perf_counter()
+    step = 256
+    for b in range(0, len(series_host), step):
+        st, coef, ll, cnt = O.fit_batch(series_host[b:b + step], p, d, q, I, smear=smear)
+        parts.append((st, coef, ll, cnt))
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    st, coef, ll, cnt = (np.concatenate([x[i] for x in parts]) for i in range(4))
+    return dict(status=st, coef=coef, ll=ll, n_eval=cnt[:, 0], n_grad=cnt[:, 1])
+
+
+def run_default_leg(args):
+    """the drop-in as a caller gets it -- arima_fit_batch_device with the ABI's default options
+    (no arima_set_option call: fit_pipeline 1, the default scheduler knobs) under the box's own GPU_MAX_HW_QUEUES, in a
+    child process that runs to completion before this process touches the GPU. Returns its JSON line (or an error)."""
+    env = dict(os.environ, SPARKTS_BENCH_DEFAULT_LEG="1")
+    if _BOX_QUEUES is None:
+        env.pop("GPU_MAX_HW_QUEUES", None)
+    else:
+        env["GPU_MAX_HW_QUEUES"] = _BOX_QUEUES
+    env.pop("SPARKTS_OPTIONS", None)
+    cmd = [sys.executable, os.path.abspath(__file__), "--default-leg-child", "--config", args.config,
+           "--series", str(args.series), "--steps", "5", "--warmup", "1"]
+    try:
+        out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
+    except subprocess.TimeoutExpired:
+        return {"error": "timeout"}
+    for line in out.stderr.splitlines():
+        log(line)
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    if out.returncode != 0 or not lines:
+        return {"error": f"exit {out.returncode}", "stderr_tail": out.stderr[-400:]}
+    return json.loads(lines[-1])
+
+
+def default_leg_child(args):
+    import torch
+    import sparkts_amd._lib as L
+    p, d, q, I, T, base, jitter = CONFIGS[args.config]
+    N, k = args.series, p + q + I
+    dev_id = int(os.environ.get("SPARKTS_DEVICE", "") or 0)
+    dev = torch.device("cuda", dev_id)
+    eng = L.Engine.get(dev_id)                  # no set_option: the ABI's defaults
+    series = torch.empty((N, T), dtype=torch.float64, device=dev)
+    eng.sample_device(series.data_ptr(), N, T, T, p, d, q, I, base, jitter, SEED, 0)
+    o = dict(coef=torch.empty((N, k), dtype=torch.float64, device=dev), ll=torch.empty(N, dtype=torch.float64, device=dev),
+             status=torch.empty(N, dtype=torch.int32, device=dev), n_eval=torch.empty(N, dtype=torch.int32, device=dev),
+             n_grad=torch.empty(N, dtype=torch.int32, device=dev), flags=torch.empty(N, dtype=torch.uint8, device=dev))
+
+    def step():
+        eng.fit_batch_device(series.data_ptr(), N, T, T, p, d, q, I, o["coef"].data_ptr(), o["ll"].data_ptr(),
+                             o["status"].data_ptr(), o["n_eval"].data_ptr(), o["n_grad"].data_ptr(),
+                             o["flags"].data_ptr(), blocking=False)
+    for _ in range(args.warmup):
+        step()
+        eng.synchronize()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    eng.synchronize()
+    torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    st = eng.stats()
+    print(json.dumps({
+        "value": N * args.steps / dt, "unit": "series fitted/sec", "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": dt / args.steps * 1e3, "series": N,
+        "options": {n: eng.get_option(n) for n in ("fit_pipeline", "merge_live", "express_blocks", "hr_grid")},
+        "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES") or "unset (HIP default: 4)",
+        "series_done": st["series_done"],
+        "kernel_ms": {"difference": st["ms_difference"], "hr_init": st["ms_hr_init"], "cg_fit": st["ms_cg_fit"]},
+        "source": "bench.py default leg: arima_fit_batch_device with the ABI's default options in a child process "
+                  "that keeps the box's hardware-queue setting (VERDICT r4 item 4a)"}), flush=True)
+
+
 def same_bits(a, b):
     """Per-row bitwise equality of two device tensors of the same shape (rows = series)."""
     import torch
@@ -238,7 +328,7 @@ def main():
     ap.add_argument("--steps", type=int, default=None, help="timed steps (default: 20 for c2/c3, 5 for c4, 2 for c5)")
     ap.add_argument("--warmup", type=int, default=None, help="untimed warmup steps (default: 3; 1 for c5)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--series", type=int, default=1 << 20, help="series per GPU (weak scaling)")
+    ap.add_argument("--series", type=int, default=0, help="series per GPU (weak scaling; 0: 1M, 10 000 for c1)")
     ap.add_argument("--total-series", type=int, default=0, help="fixed total series over all GPUs (strong scaling)")
     ap.add_argument("--smear", type=int, default=1, choices=[0, 1])
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline sample budget (0 = skip)")
@@ -247,7 +337,8 @@ def main():
                     help="fit contexts (0: 6, or 4 for c4, whose 1M x 4096 fit then stays one slice of free HBM)")
     ap.add_argument("--express-blocks", type=int, default=-1, help="express workgroups of the fit kernel (-1: CUs/16)")
     ap.add_argument("--e2e", type=int, default=1, choices=[0, 1])
-    ap.add_argument("--fit-kernel", type=int, default=-1, help="0: k_cg_fit (LDS slots), 2: rounds of streaming passes; -1: default")
+    ap.add_argument("--default-leg", type=int, default=1, choices=[0, 1])
+    ap.add_argument("--default-leg-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--device", type=int, default=None, help="GPU of every rank (default: LOCAL_RANK's)")
     ap.add_argument("--search-lanes", type=int, default=0,
                     help="c5: concurrent search lanes (0: 12; 8 / 10 / 12 / 16 / 24 lanes: 18.1 / 20.3 / 21.3 / 19.5 / "
@@ -256,6 +347,10 @@ def main():
     args = ap.parse_args()
     if args.device is not None:
         os.environ["SPARKTS_DEVICE"] = str(args.device)
+    if args.series <= 0:
+        args.series = DEFAULT_SERIES.get(args.config, 1 << 20)
+    if args.default_leg_child:
+        return default_leg_child(args)
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
@@ -303,11 +398,8 @@ def main():
 
     if args.dry_run:
         barrier()
-        shards = [None] * world
-        if world > 1:
-            dist.all_gather_object(shards, (first, last))
-        else:
-            shards = [(first, last)]
+        from sparkts_amd.sharding import gather_results
+        shards = gather_results([np.array([[first, last]], dtype=np.int64)], dist if world > 1 else None)[0].tolist()
         if rank == 0:
             print(json.dumps({"dry_run": True, "n_gpus": world, "scaling": scaling, "total_series": total_series,
                               "shards": shards}), flush=True)
@@ -316,14 +408,17 @@ def main():
             dist.destroy_process_group()
         return
 
+    # the drop-in as a caller gets it: ABI defaults in a child process that keeps the box's
+    # hardware-queue setting, run to completion BEFORE this process touches the GPU
+    default_leg = None
+    if args.config == "c2" and world == 1 and args.default_leg:
+        default_leg = run_default_leg(args)
     import sparkts_amd._lib as L
     dev = torch.device("cuda", dev_id)
     eng = L.Engine.get(dev_id)
     eng.set_option("smear", args.smear)
     eng.set_option("fit_pipeline", args.pipeline)
     eng.set_option("express_blocks", args.express_blocks)
-    if args.fit_kernel >= 0:
-        eng.set_option("fit_kernel", args.fit_kernel)
     if args.grid_blocks:
         eng.set_option("grid_blocks", args.grid_blocks)
     if args.config == "c5":
@@ -417,16 +512,35 @@ def main():
     # HBM bytes the fit kernel streams by construction: one series row per served lane-pass
     passes_bytes = (served + s0["express_series"]) * n * 8.0
 
+    # oracle parity of the timed step on EVERY rank: each rank fits the first rows of its own shard
+    # with the CPU restatement (bounded by --cpu-seconds) and the verdicts meet in gloo min / sum reductions
+    cpu = None
+    rows_checked, rows_ok = 0, 0
+    if args.cpu_seconds > 0 and N > 0:
+        cap = 1024 if args.config == "c4" else 4096
+        host = series[: min(N, cap)].cpu().numpy()
+        if world == 1:
+            exp, cpu = cpu_baseline(host, p, d, q, I, args.smear, args.cpu_seconds)
+        else:
+            exp = oracle_rows(host, p, d, q, I, args.smear, args.cpu_seconds)
+        rows_checked = len(exp["status"])
+        res = {k_: v[:rows_checked].cpu().numpy() for k_, v in last.items()}
+        exp["pqi"] = (p, q, int(I))
+        rows_ok = oracle_row_parity(res, exp)
+        if rows_ok != rows_checked:
+            log(f"[rank {rank}] PARITY: {rows_checked - rows_ok} of {rows_checked} oracle rows differ from the timed step")
+    from sparkts_amd.sharding import parity_over_ranks
+    node_parity = parity_over_ranks(rows_ok, rows_checked, dist if world > 1 else None)
+
     if rank == 0:
         sha = build_sha()
         # the record key names the fit kernel and any non-default engine options too: a record of another variant
         # never stands for this run's kernel
         pmc, pmc_key = pmc_traffic({"series": N, "T": T, "p": p, "d": d, "q": q, "I": int(I), "smear": args.smear,
-                                    "fit_kernel": eng_fit_kernel(eng),
+                                    "fit_kernel": 0,
                                     "options": os.environ.get("SPARKTS_OPTIONS", "")}, sha)
         result = {
-            "metric": "series fitted/sec, ARIMA(2,1,2) CSS-CGD, 1M x 1024 pts" if args.config == "c2"
-            else f"series fitted/sec, {args.config}",
+            "metric": METRICS.get(args.config, f"series fitted/sec, {args.config}"),
             "value": total_series * args.steps / elapsed,
             "unit": "series fitted/sec",
             "n_gpus": world,
@@ -440,12 +554,14 @@ def main():
             "data": f"synthetic: ARIMAModel.sample semantics on device, seed {SEED}, coef jitter +-{jitter}",
             "config": {"workload": f"ARIMA({p},{d},{q}){'+c' if I else ''} css-cgd, "
                                    + (f"{total_series} series total over {world} GPU(s)" if scaling == "strong"
-                                      else f"{N} series x {T} pts per GPU") + " (BASELINE.json configs[1]/[2])",
+                                      else f"{N} series x {T} pts per GPU")
+                                   + {"c1": " (BASELINE.json configs[0])", "c4": " (BASELINE.json configs[3])"}.get(
+                                       args.config, " (BASELINE.json configs[1]/[2])"),
                        "series_per_gpu": N, "series_total": total_series, "series_len": T,
                        "parallelism": f"series-sharded x{world}, no collective",
                        "breeze_overlap": "smear" if args.smear else "shift",
-                       "fit_kernel": "rounds (k_rounds_pass / k_rounds_advance, then k_cg_fit on the tail)"
-                       if eng_fit_kernel(eng) == 2 else "k_cg_fit (LDS slots, 1 wave/SIMD)",
+                       "fit_kernel": "k_cg_fit (LDS slots, 1 wave/SIMD)", "fit_pipeline": args.pipeline,
+                       "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                        "converged_fraction": conv, "series_done": s0["series_done"],
                        "mean_n_eval": s0["n_eval"] / max(N, 1), "mean_n_grad": s0["n_grad"] / max(N, 1),
                        "lane_f_passes_per_series": s0["f_passes"] / max(N, 1),
@@ -487,25 +603,22 @@ def main():
                          "merge": {"series": s0.get("merge_series"), "waves": s0.get("merge_waves")},
                          "wave_passes": {"f": s0["wave_f_passes"], "g": s0["wave_g_passes"],
                                          "multi": s0["wave_multi_passes"]}},
-            "cpu_baseline": None,
+            "cpu_baseline": cpu,
         }
+        if default_leg is not None:
+            result["default_config"] = default_leg
         if world == 1 and args.e2e:
             result["end_to_end_host"] = end_to_end(eng, series, p, d, q, I)
         parity = {"configuration": f"the last timed step: fit_pipeline {args.pipeline} on GPU_MAX_HW_QUEUES="
                                    f"{os.environ.get('GPU_MAX_HW_QUEUES')}",
                   "vs_isolated": iso_mismatch == 0, "isolated_mismatch_series": iso_mismatch,
-                  "isolated_compared_series": total_series, "oracle_rows": 0, "bit_identical": None}
-        if world == 1 and args.cpu_seconds > 0:
-            host = series[: 4096].cpu().numpy()
-            exp, result["cpu_baseline"] = cpu_baseline(host, p, d, q, I, args.smear, args.cpu_seconds)
-            rows = len(host)
-            res = {k: v[:rows].cpu().numpy() for k, v in last.items()}
-            exp["pqi"] = (p, q, int(I))
-            parity["oracle_rows"] = rows
-            parity["bit_identical"] = oracle_row_parity(res, exp)
-            parity["oracle_source"] = "oracle/arima_oracle.c on rows 0..%d (the cpu_baseline sample)" % (rows - 1)
-            if parity["bit_identical"] != rows:
-                log(f"PARITY: {rows - parity['bit_identical']} of {rows} oracle rows differ from the timed step")
+                  "isolated_compared_series": total_series,
+                  "oracle_rows": node_parity["oracle_rows"], "bit_identical": node_parity["bit_identical"],
+                  "ranks_checked": node_parity["ranks"],
+                  "every_rank_bit_identical": node_parity["every_rank_bit_identical"],
+                  "min_rank_fraction": node_parity["min_rank_fraction"],
+                  "oracle_source": "oracle/arima_oracle.c on the first rows of every rank's shard (rank 0: the "
+                                   "cpu_baseline sample), gloo sum / min over ranks"}
         result["parity"] = parity
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -123,10 +123,8 @@ int         arima_synchronize(arima_handle *h);
 /* Tuning knobs (not part of the reference contract): "smear" (Breeze reading at ARIMA.scala:526, default 1),
  * "fit_pipeline" (fit contexts in rotation for *_device fits, 1..8, default 1), "host_chunk" / "host_pipeline"
  * (series per chunk and contexts of the chunked host path, default 262144 / 3), "express_blocks",
- * "grid_blocks", "search_lanes" (in-kernel scheduler and order-search concurrency), "fit_kernel" (0: k_cg_fit with
- * LDS-resident optimizer slots; 2: rounds of streaming passes, then k_cg_fit on the last series; 3: k_cg_fit_r, two
- * waves per SIMD with one optimizer slot per lane in registers, rows up to cg_fit_reg_max_n), "rounds_max",
- * "rounds_tail", "rounds_pass_waves" (fit_kernel 2), "hr_grid" (k_hr_init grid: 0 = a lane per series, > 0 = that
+ * "grid_blocks", "search_lanes" (in-kernel scheduler and order-search concurrency), "hr_grid" (k_hr_init grid:
+ * 0 = a lane per series, > 0 = that
  * many single-wave workgroups, -1 = 1024 for pipelined fits else 0), "fit_slice_bytes"
  * (differenced workspace of one slice of a large device fit), "express_ring" (express hand-offs per launch),
  * "row_pad" (doubles added to the stride of the differenced-row workspaces, whole 128-B lines, default 0),
@@ -138,10 +136,6 @@ int         arima_synchronize(arima_handle *h);
 int         arima_set_option(arima_handle *h, const char *name, int64_t value);
 /* Current value of a tuning knob (the names arima_set_option takes); ARIMA_E_INVALID_ARG for an unknown name. */
 int         arima_get_option(const arima_handle *h, const char *name, int64_t *value);
-/* Diagnostics (fit_kernel 2): waits for the last device fit and copies its round-control words (per round: the
- * request counts of lists G, F+2, F+1, F+0 and the pass kernel's tile counter, 8 words a round; the tail count
- * after the last round) into out[0 .. max_words). Returns the number of words written, or a negative error. */
-int         arima_rounds_trace(arima_handle *h, unsigned *out, int max_words);
 
 /* ---- ARIMA.fitModel over a batch (ARIMA.scala:79-116) ----------------------------------------------- *
  * series    N x T host, series-major                 user_init  NULL (Hannan-Rissanen, ARIMA.scala:216) or N x k

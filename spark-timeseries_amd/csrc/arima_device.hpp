@@ -158,16 +158,10 @@ __device__ __forceinline__ void stream_elems(const double *__restrict__ row, int
 // ASCENDING i, so after every update positions 1..q-1 all equal the previous errs(0): maTerms is
 // [e_{t-1}, e_{t-2}, e_{t-2}, ...] (a smear for q >= 3, exactly what the reference computes).
 // ------------------------------------------------------------------------------------------------------
-#ifndef STS_PREFETCH_F
-#define STS_PREFETCH_F 3
-#endif
-#ifndef STS_PREFETCH_G
-#define STS_PREFETCH_G 1
-#endif
 // (round 4: 4 / 2 -> 3 / 1 on one box: pipelined C2 9.47-9.59 -> 10.47-10.58 M series/s, isolated launch 138.5 ->
 // 128.6 ms, profiles/r04/p_pf; registers and scratch of k_cg_fit unchanged -- the F pass's inner loop schedules better)
-constexpr int kPrefetchF = STS_PREFETCH_F;   // chunks in flight per lane in objective passes
-constexpr int kPrefetchG = STS_PREFETCH_G;   // ... in gradient passes (5x the VALU work per byte)
+constexpr int kPrefetchF = 3;   // chunks in flight per lane in objective passes
+constexpr int kPrefetchG = 1;   // ... in gradient passes (5x the VALU work per byte)
 
 // Full pass. G = false: objective only -> css. G = true: also gradientlogLikelihoodCSSARMA -> g[] (already
 // divided by -sigma2, :532). SMEAR selects the Breeze overlap semantics of :526 (false = row shift).
@@ -691,10 +685,7 @@ __device__ __forceinline__ void grad_column_lds(const double *row, int n,
 // first_elem(r) (series index of the element that completes row r), push(v, x, y) (next row from the next
 // series element).
 // ------------------------------------------------------------------------------------------------------
-#ifndef STS_HR_PF
-#define STS_HR_PF 2
-#endif
-constexpr int kPrefetchHR = STS_HR_PF;   // 128-B chunks in flight per lane in the Householder passes
+constexpr int kPrefetchHR = 2;   // 128-B chunks in flight per lane in the Householder passes
 
 template <int C>
 struct HouseholderState {

@@ -103,14 +103,8 @@ __global__ __launch_bounds__(256) void k_inverse_difference(const double *__rest
 // =======================================================================================================
 constexpr int kFcMaxOrder = 5;   // p, q <= 5 (check_orders)
 constexpr int kFcMaxD = 8;
-#ifndef STS_FC_NT
-#define STS_FC_NT 0                                                   // non-temporal tile loads / flush stores
-#endif
-#ifndef STS_FC_CH
-#define STS_FC_CH 32
-#endif
 constexpr int kFcWave = 64;
-constexpr int kFcCh = STS_FC_CH;                                     // time steps per tile
+constexpr int kFcCh = 32;                                            // time steps per tile
 constexpr int kFcRing = kFcCh + kFcMaxD;                             // LDS ring columns (>= kFcCh + kFcMaxD)
 constexpr int kFcRowsPerLd = kFcWave / kFcCh;                        // rows per coalesced load instruction
 static_assert(kFcRing >= kFcCh + kFcMaxD, "output ring too small");
@@ -171,11 +165,7 @@ __global__ __launch_bounds__(kFcWave) void k_forecast(const double *__restrict__
 #pragma unroll
         for (int j = 0; j < kFcCh; ++j) {
             const int64_t gi = row0 + j * kFcRowsPerLd + tr;
-#if STS_FC_NT
-            pf[j] = __builtin_nontemporal_load(ts_all + (gi < N ? gi : N - 1) * ld_in + t);
-#else
             pf[j] = ts_all[(gi < N ? gi : N - 1) * ld_in + t];
-#endif
         }
     };
     int flushed = 0;                                                   // [0, flushed) is in HBM
@@ -265,12 +255,7 @@ __global__ __launch_bounds__(kFcWave) void k_forecast(const double *__restrict__
 #pragma unroll
                 for (int j = 0; j < kFcCh; ++j) {
                     const int r = j * kFcRowsPerLd + tr;
-#if STS_FC_NT
-                    if (row0 + r < N)
-                        __builtin_nontemporal_store(ring[r][idx % kFcRing], out_all + (row0 + r) * ld_out + idx);
-#else
                     if (row0 + r < N) out_all[(row0 + r) * ld_out + idx] = ring[r][idx % kFcRing];
-#endif
                 }
             }
             flushed = fe;
@@ -622,32 +607,17 @@ int launch_cg_fit(const double *y, int64_t ld, int n, int64_t N, int p, int q, i
                   const double *init, const int32_t *init_status, double *coef_out, double *ll_out,
                   int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
                   unsigned long long *ctl, int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready,
-                  int join_express, int variant, const FitRounds *rounds, hipStream_t s) {
+                  int join_express, hipStream_t s) {
     if (N == 0) return ARIMA_OK;
 #define C_(PP)                                                                                             \
     launch_cg_fit_P<PP>(y, ld, n, N, q, I, smear, init, init_status, coef_out, ll_out, status_out, n_eval_out, \
-                        n_grad_out, flags_out, ctl, grid_blocks, express_blocks, xq, xready, join_express, variant, \
-                        rounds, s)
+                        n_grad_out, flags_out, ctl, grid_blocks, express_blocks, xq, xready, join_express, s)
     STS_P_SWITCH(C_)
 #undef C_
 }
 
-int cg_fit_reg_max_n(int k) {
-#if !STS_REG_KERNEL
-    (void)k;
-    return -1;                                   // not built: every fit keeps k_cg_fit
-#else
-    switch (k) {
-#define K_(KK) case KK: return express_max_n<KK>(reg_wave_lds_bytes<KK>());
-        K_(1) K_(2) K_(3) K_(4) K_(5) K_(6) K_(7) K_(8) K_(9) K_(10) K_(11)
-#undef K_
-    default: return 0;
-    }
-#endif
-}
-
-int cg_fit_series_per_block(int p, int q, int I, int variant) {
-#define C_(PP) cg_fit_series_per_block_P<PP>(q, I, variant)
+int cg_fit_series_per_block(int p, int q, int I) {
+#define C_(PP) cg_fit_series_per_block_P<PP>(q, I)
     STS_P_SWITCH(C_)
 #undef C_
 }
@@ -678,20 +648,4 @@ int launch_model_flags(const double *coef, int64_t N, int p, int q, int I, uint8
 int hr_shape_status_host(int n, int p, int q, int I) { return hr_shape_status(n, p, q, I); }
 int ar_shape_status_host(int n, int p, int I) { return ar_shape_status(n, p, I); }
 
-}  // namespace sts
-
-namespace sts {
-int rounds_rec_bytes(int k) {
-    switch (k) {
-#define RC_(KK) case KK: return rounds_rec_stride<KK>();
-        RC_(1) RC_(2) RC_(3) RC_(4) RC_(5) RC_(6) RC_(7) RC_(8) RC_(9) RC_(10) RC_(11)
-#undef RC_
-    default: return 0;
-    }
-}
-int rounds_resp_words(int k) { return k >= 1 && k <= 11 ? 1 + spec_ns<5>() + k : 0; }
-}  // namespace sts
-
-namespace sts {
-int64_t rounds_ranges(int64_t N) { return (N + kRangeSeries - 1) / kRangeSeries; }
 }  // namespace sts

@@ -208,28 +208,10 @@ struct alignas(8) FitSlot {
 };
 
 constexpr int kFitWaves = kFitBlockWaves;    // waves per workgroup (arima_launch.hpp)
-#ifndef STS_F_RIDE
-#define STS_F_RIDE 1
-#endif
-constexpr bool kFRide = STS_F_RIDE != 0;     // objective requests fill the idle lanes of gradient passes
-#ifndef STS_OLD_EVALS
-#define STS_OLD_EVALS 128
-#endif
-constexpr int kOldEvals = STS_OLD_EVALS;     // evaluations after which a series is served with priority
-#ifndef STS_NCH_CHOICE
-#define STS_NCH_CHOICE 1
-#endif
-constexpr bool kNchChoice = STS_NCH_CHOICE != 0;   // objective pass width chosen by evaluations per cost
-#ifndef STS_CHAIN_OVERHEAD16
-#define STS_CHAIN_OVERHEAD16 6
-#endif
-constexpr int kChainOverhead16 = STS_CHAIN_OVERHEAD16;   // per-step streaming cost of a pass, in 1/16 chains
-#ifndef STS_ADV_REGS
-#define STS_ADV_REGS 0                       // bulk optimizer steps on a register copy of the LDS slot (A/B: DESIGN 7.2)
-#endif
-#ifndef STS_ADV_REGS_X
-#define STS_ADV_REGS_X 0                     // ... and the express waves' (measured slower: profiles/r03/v_adv)
-#endif
+constexpr bool kFRide = true;                // objective requests fill the idle lanes of gradient passes
+constexpr int kOldEvals = 128;               // evaluations after which a series is served with priority
+constexpr bool kNchChoice = true;            // objective pass width chosen by evaluations per cost
+constexpr int kChainOverhead16 = 6;          // per-step streaming cost of a pass, in 1/16 chains
 
 constexpr int kFitLdsBudget = 160 * 1024 - 1024;
 // slots per wave: as many as the LDS holds, at most 2 per lane, a multiple of 8 (at least 64 unless more than
@@ -259,14 +241,8 @@ constexpr int fit_slots_per_wave() {
 // an entry's tag read stale for 20 s while its ready word had moved on).
 constexpr int kExpressRing = kExpressRingEntries;
 constexpr int kExpressEntryBytes = 512;      // ring stride reserved per entry (>= sizeof(FitSlotCore<K>) for K <= 11)
-#ifndef STS_EXPRESS_GROUPS
-#define STS_EXPRESS_GROUPS 1
-#endif
-constexpr int kExpressGroups = STS_EXPRESS_GROUPS;   // series per express wave (at most; LDS permitting)
-#ifndef STS_DONATE_EVALS
-#define STS_DONATE_EVALS 256
-#endif
-constexpr int kDonateEvals = STS_DONATE_EVALS;   // a slot is donated only after this many evaluations ...
+constexpr int kExpressGroups = 1;            // series per express wave (2 and 4 measured slower)
+constexpr int kDonateEvals = 256;            // a slot is donated only after this many evaluations ...
 constexpr int kDonateEvalsDrained = 32;      // ... or this many once the batch's work counter has run out
 
 template <int K>
@@ -379,35 +355,21 @@ __device__ __forceinline__ void record_fault(unsigned long long *ctl, unsigned l
 }
 
 
-#ifndef STS_PIT
-#define STS_PIT 1
-#endif
-constexpr bool kPit = STS_PIT != 0;          // express objective passes parallel in time (css_pit_lds)
-
-#ifndef STS_PIT_G
-#define STS_PIT_G 1
-#endif
+constexpr bool kPit = true;                  // express objective passes parallel in time (css_pit_lds)
 constexpr int kPitGMaxK = 12;                // gradient passes parallel in time (in column chunks of 6) for K <= this
 
-template <int P, int Q, int I, bool SMEAR, int PIT_BMAX = 16, bool PIT_G = STS_PIT_G != 0>
+template <int P, int Q, int I, bool SMEAR, int PIT_BMAX = 16, bool PIT_G = true>
 __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__restrict__ y, int64_t ld, int n,
                             double *__restrict__ coef_out, double *__restrict__ ll_out,
                             int32_t *__restrict__ status_out, int32_t *__restrict__ n_eval_out,
                             int32_t *__restrict__ n_grad_out, uint8_t *__restrict__ flags_out,
                             unsigned long long *__restrict__ ctl, unsigned char *__restrict__ xq,
-                            unsigned *__restrict__ xready, int64_t N, int lane,
-                            const int32_t *__restrict__ direct_list = nullptr,
-                            const unsigned char *__restrict__ direct_rec = nullptr) {
-    // direct mode (direct_list != nullptr, the tail of a rounds fit): no bulk waves and no ring -- a group claims the
-    // next listed series from the work counter ctl[0] (N = the list's length) and loads its optimizer state from
-    // its record in direct_rec; up to 4 series per wave (each group needs K <= 16 lanes for the gradient columns)
+                            unsigned *__restrict__ xready, int64_t N, int lane) {
     constexpr int K = I + P + Q;
     constexpr int NS = spec_ns<K>();
-    const bool direct = direct_list != nullptr;
     const int gbytes = express_group_bytes<K>(n);
     int XG = lds_bytes / gbytes;
-    if (direct) XG = XG >= 4 ? 4 : (XG >= 2 ? 2 : 1);
-    else XG = XG >= kExpressGroups ? kExpressGroups : (XG >= 2 ? 2 : 1);
+    XG = XG >= kExpressGroups ? kExpressGroups : (XG >= 2 ? 2 : 1);
     const int GL = 64 / XG;                                 // lanes per group
     const int grp = lane / GL, gl = lane % GL;
     const bool glead = gl == 0;
@@ -425,7 +387,7 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
     unsigned long long tk_time = 0, tk_polls = 0;          // fault diagnostics: this ticket's age and polls,
     unsigned tk_rfirst = 0, tk_rmax = 0;                    // first / largest ready word seen
     if (glead) {
-        ticket = add_agent(direct ? &ctl[0] : &ctl[20], 1ull);
+        ticket = add_agent(&ctl[20], 1ull);
         tk_time = __builtin_amdgcn_s_memrealtime();
     }
     ticket = __shfl(ticket, grp * GL);
@@ -433,9 +395,7 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
     for (;;) {
         // ---- groups waiting on a ticket: poll (group leader), then load the entry (whole group) ----
         int arrived = 0;
-        if (direct) {
-            if (gstate == 0) arrived = ticket < (unsigned long long)N ? 1 : 2;
-        } else if (gstate == 0 && glead) {
+        if (gstate == 0 && glead) {
             const unsigned e = (unsigned)(ticket % xring);
             const unsigned long long *ent = reinterpret_cast<const unsigned long long *>(xq + (size_t)e * kExpressEntryBytes);
             // poll the ready word; every 32nd poll reads it at the memory side
@@ -483,16 +443,7 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
         arrived = __shfl(arrived, grp * GL);
         if (arrived == 2) gstate = 2;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (arrived == 1 && direct) {
-            using DLane = CGLane<K, NS, spec_nc<K>()>;
-            const int64_t dsid = direct_list[ticket];
-            const unsigned long long *src = reinterpret_cast<const unsigned long long *>(
-                direct_rec + dsid * (int64_t)((sizeof(DLane) + 127) / 128 * 128));
-            constexpr int W = (int)(sizeof(DLane) / 8);
-            static_assert(sizeof(DLane) % 8 == 0, "8-byte words");
-            for (int w = gl; w < W; w += GL) reinterpret_cast<unsigned long long *>(&ES.s)[w] = src[w];
-            if (glead) ES.sid = dsid;
-        } else if (arrived == 1) {
+        if (arrived == 1) {
             const unsigned e = (unsigned)(ticket % xring);
             const unsigned long long *src = reinterpret_cast<const unsigned long long *>(xq + (size_t)e * kExpressEntryBytes);
             constexpr int W = (int)(sizeof(FitSlotCore<K>) / 8);
@@ -596,11 +547,7 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
         if (req == REQ_G && glead) xch[K] = css_to_loglik(cssv, n);
         wave_sync_lds();
         if (glead && req != REQ_NONE) {
-#if STS_ADV_REGS_X
-            CGLane<K, NS, spec_nc<K>()> L = ES.s;           // the long series' critical path: state in registers
-#else
             CGLane<K, NS, spec_nc<K>()> &L = ES.s;
-#endif
             if (req == REQ_F) {
                 for (int h = 1; h <= nsp && h <= NS; ++h) L.spec_store(h - 1, xch[h]);
                 double g0[K];
@@ -617,9 +564,6 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
                 L.advance(xch[K], g);
                 pg++;
             }
-#if STS_ADV_REGS_X
-            ES.s = L;
-#endif
         }
         wave_sync_lds();
         // ---- finished series: write the result, take a new ticket ----
@@ -636,7 +580,7 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
             grads += ES.s.n_grad;
             hits += ES.s.spec_hits;
             done++;
-            ticket = add_agent(direct ? &ctl[0] : &ctl[20], 1ull);
+            ticket = add_agent(&ctl[20], 1ull);
             tk_time = __builtin_amdgcn_s_memrealtime();
             tk_polls = 0;
             tk_rfirst = tk_rmax = 0;
@@ -665,10 +609,7 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
     const int32_t *__restrict__ init_status, double *__restrict__ coef_out, double *__restrict__ ll_out,
     int32_t *__restrict__ status_out, int32_t *__restrict__ n_eval_out, int32_t *__restrict__ n_grad_out,
     uint8_t *__restrict__ flags_out, unsigned long long *__restrict__ ctl, unsigned char *__restrict__ xq,
-    unsigned *__restrict__ xready, int n_bulk, int join_express, const int32_t *__restrict__ resume_list,
-    const unsigned *__restrict__ resume_n, const unsigned char *__restrict__ resume_rec) {
-    // resume_list != nullptr: the launch fits the *resume_n series listed there from their optimizer states in
-    // resume_rec (the records of arima_fit_rounds.hpp; init / init_status unused) instead of series 0..N-1.
+    unsigned *__restrict__ xready, int n_bulk, int join_express) {
     // ctl[0] = work counter, ctl[1] = lane F passes, ctl[2] = lane G passes, ctl[3] = wave F passes (one chain),
     // ctl[4] = wave G passes, ctl[5] = objective evaluations, ctl[6] = gradient evaluations, ctl[7] = spec hits,
     // ctl[8] = wave F passes with speculative chains, ctl[9] = speculative chains evaluated,
@@ -684,13 +625,6 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
     __shared__ int assign[kFitWaves][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const bool has_express = n_bulk < (int)gridDim.x;
-    if (resume_list) N = (int64_t)*resume_n;             // written by the previous kernel (stream order)
-    if (resume_list && n_bulk == 0) {                     // the tail of a rounds fit, every wave on the express path
-        fit_express<P, Q, I, SMEAR>(reinterpret_cast<unsigned char *>(&slots[wave][0]), (int)sizeof(slots[0]), y, ld,
-                                    n, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out, ctl, xq,
-                                    xready, N, lane, resume_list, resume_rec);
-        return;
-    }
     if ((int)blockIdx.x >= n_bulk) {                      // express workgroup: this wave's share of the LDS
         fit_express<P, Q, I, SMEAR>(reinterpret_cast<unsigned char *>(&slots[wave][0]), (int)sizeof(slots[0]), y, ld,
                                     n, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out, ctl, xq,
@@ -711,7 +645,7 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
     // A wave reserves entries and leaves the active count in one CAS, and leaves without entries only by a CAS that
     // sees every reserved entry claimed -- so while entries are unclaimed some active wave remains to take them.
     // Only where a series is fitted changes, never its result.
-    const int merge_live = resume_list ? 0 : (int)ctl[44];
+    const int merge_live = (int)ctl[44];
     unsigned char *mpool = xq + (size_t)(kExpressRing - kMergeCap) * kExpressEntryBytes;
     unsigned *mready = xready + (kExpressRing - kMergeCap);
     unsigned long long merge_head = 0;     // entries claimed, as last seen (a lower bound)
@@ -756,16 +690,6 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
 #endif
                     S.sid = -1;
                     S.s.req = REQ_NONE;
-                    need = false;
-                } else if (resume_list) {             // a series of the rounds, with its request posted
-                    const int64_t rs = resume_list[sid];
-                    S.s = *reinterpret_cast<const CGLane<K, NS, spec_nc<K>()> *>(
-                        resume_rec + rs * (int64_t)((sizeof(CGLane<K, NS, spec_nc<K>()>) + 127) / 128 * 128));
-                    S.sid = rs;
-#ifdef STS_TIMING
-                    S.t_start = (double)__builtin_amdgcn_s_memrealtime();
-                    S.t_donate = 0.0;
-#endif
                     need = false;
                 } else {
                     const int st0 = init_status ? init_status[sid] : ARIMA_ST_OK;
@@ -1110,19 +1034,9 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
 #endif
         bool need = false;
         if (served) {
-#if STS_ADV_REGS
-            // the state machine runs on a register copy of the slot: inside advance() every field access would
-            // otherwise be an LDS access whose latency one wave per SIMD cannot hide
-            CGLane<K, NS, spec_nc<K>()> L = S.s;
-#else
             CGLane<K, NS, spec_nc<K>()> &L = S.s;
-#endif
             L.req = REQ_NONE;
-#if STS_ADV_REGS == 2
-            L.step(resp_f, g);                    // force-inlined on the register copy (A/B)
-#else
             L.advance(resp_f, g);
-#endif
             if (L.done()) {
                 double pt[K];
 #pragma unroll
@@ -1137,9 +1051,6 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
                 done++;
                 need = true;
             }
-#if STS_ADV_REGS
-            S.s = L;
-#endif
         }
 #ifdef STS_TIMING
         const unsigned long long t_s = now();
@@ -1274,14 +1185,6 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
 
 }  // namespace sts
 
-#include "arima_fit_rounds.hpp"
-#ifndef STS_REG_KERNEL
-#define STS_REG_KERNEL 0                     // fit_kernel 3 (k_cg_fit_r) is built only on request: measured slower
-#endif
-#if STS_REG_KERNEL
-#include "arima_fit_reg.hpp"
-#endif
-
 namespace sts {
 
 // =======================================================================================================
@@ -1411,88 +1314,30 @@ int launch_ar_fit_P(const double *y, int64_t ld, int n, int64_t N, int I, double
 }
 
 // k_cg_fit launcher for one AR order and Breeze reading (each instantiated in its own translation unit,
-// arima_cg_p<P>_s<S>.hip, so the build parallelises over the heaviest kernel). variant 0: k_cg_fit (LDS slots, one
-// wave per SIMD); variant 2: rounds of streaming passes (arima_fit_rounds.hpp) until few series are left, then
-// k_cg_fit resumes those from their records.
+// arima_cg_p<P>_s<S>.hip, so the build parallelises over the heaviest kernel).
 template <int P, bool S>
 int launch_cg_fit_PS(const double *y, int64_t ld, int n, int64_t N, int q, int I, const double *init,
                      const int32_t *init_status, double *coef_out, double *ll_out, int32_t *status_out,
                      int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out, unsigned long long *ctl,
                      int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready, int join_express,
-                     int variant, const FitRounds *rounds, hipStream_t s) {
+                     hipStream_t s) {
     return with_order(q, [&](auto Qc) {
         return with_bool(I, [&](auto Ic) {
-            {
-                constexpr int Q = decltype(Qc)::value, II = decltype(Ic)::value;
-                constexpr int K = P + Q + II;
-                if constexpr (K == 0) {
-                    return ARIMA_E_INVALID_ARG;
-                } else {
-                    constexpr int SPW = fit_slots_per_wave<K>();
-#if STS_REG_KERNEL
-                    if (variant == 3) {                   // two waves per SIMD, register slots (arima_fit_reg.hpp)
-                        constexpr int SPL = reg_lds_slots<K>();
-                        if (n > express_max_n<K>(reg_wave_lds_bytes<K>())) express_blocks = 0;
-                        hipLaunchKernelGGL((k_cg_fit_r<P, Q, II, S, SPL>), dim3(grid_blocks + express_blocks), dim3(64),
-                                           0, s, y, ld, n, N, init, init_status, coef_out, ll_out, status_out,
-                                           n_eval_out, n_grad_out, flags_out, ctl, xq, xready, grid_blocks,
-                                           join_express, nullptr, nullptr, nullptr);
-                        STS_CHECK_LAUNCH();
-                        return ARIMA_OK;
-                    }
-#else
-                    if (variant == 3) return ARIMA_E_UNSUPPORTED;
-#endif
-                    // express blocks only when the row fits next to the state in one wave's LDS share
-                    const int lds_per_wave = SPW * (int)sizeof(FitSlot<K>);
-                    if (n > express_max_n<K>(lds_per_wave)) express_blocks = 0;
-                    const int32_t *resume_list = nullptr;
-                    const unsigned *resume_n = nullptr;
-                    const unsigned char *resume_rec = nullptr;
-                    if (variant == 2) {                   // rounds of streaming passes, then k_cg_fit on the rest
-                        if (!rounds || rounds->max_rounds < 1) return ARIMA_E_INVALID_ARG;
-                        const FitRounds &R = *rounds;
-                        unsigned *tail_n = R.rc + (size_t)(R.max_rounds + 1) * kRcStride;
-                        const int nranges = (int)((N + kRangeSeries - 1) / kRangeSeries);
-                        auto compact = [&](int ro) {       // marks -> round ro's lists (+ the tail list)
-                            hipLaunchKernelGGL(k_rounds_count, dim3(nranges), dim3(64), 0, s, N, R.mark, R.counts);
-                            hipLaunchKernelGGL(k_rounds_scan, dim3(1), dim3(1024), 0, s, nranges, R.counts,
-                                               R.rc + (size_t)ro * kRcStride, tail_n);
-                            hipLaunchKernelGGL(k_rounds_scatter, dim3(nranges), dim3(64), 0, s, N, R.mark, R.counts,
-                                               R.lists + (size_t)(ro & 1) * kRoundLists * N, R.tail);
-                        };
-                        hipLaunchKernelGGL((k_rounds_init<K>), dim3(grid_for(N, 64)), dim3(64), 0, s, N, init,
-                                           init_status, R.rec, R.mark, coef_out, ll_out, status_out, n_eval_out,
-                                           n_grad_out, flags_out, ctl);
-                        compact(0);
-                        STS_CHECK_LAUNCH();
-                        for (int r = 0; r < R.max_rounds; ++r) {
-                            hipLaunchKernelGGL((k_rounds_pass<P, Q, II, S>), dim3(R.pass_blocks), dim3(64), 0, s, r, y,
-                                               ld, n, N, R.rec, R.resp, R.lists, R.rc, ctl);
-                            STS_CHECK_LAUNCH();
-                            hipLaunchKernelGGL((k_rounds_advance<P, Q, II>), dim3(R.advance_blocks), dim3(64), 0, s, r,
-                                               r == R.max_rounds - 1 ? 1 : 0, R.tail_at, N, R.rec, R.resp, R.lists,
-                                               R.rc, R.mark, coef_out, ll_out, status_out, n_eval_out, n_grad_out,
-                                               flags_out, ctl);
-                            compact(r + 1);
-                            STS_CHECK_LAUNCH();
-                        }
-                        resume_list = R.tail;
-                        resume_n = tail_n;
-                        resume_rec = R.rec;
-                        if (R.tail_express && n <= express_max_n<K>(lds_per_wave)) {
-                            // every workgroup an express wave claiming tail series directly (no bulk, no ring)
-                            express_blocks += grid_blocks;
-                            grid_blocks = 0;
-                        }
-                    }
-                    hipLaunchKernelGGL((k_cg_fit<P, Q, II, S, SPW>), dim3(grid_blocks + express_blocks),
-                                       dim3(64 * kFitWaves), 0, s, y, ld, n, N, init, init_status, coef_out, ll_out,
-                                       status_out, n_eval_out, n_grad_out, flags_out, ctl, xq, xready, grid_blocks,
-                                       join_express, resume_list, resume_n, resume_rec);
-                    STS_CHECK_LAUNCH();
-                    return ARIMA_OK;
-                }
+            constexpr int Q = decltype(Qc)::value, II = decltype(Ic)::value;
+            constexpr int K = P + Q + II;
+            if constexpr (K == 0) {
+                return ARIMA_E_INVALID_ARG;
+            } else {
+                constexpr int SPW = fit_slots_per_wave<K>();
+                // express blocks only when the row fits next to the state in one wave's LDS share
+                const int lds_per_wave = SPW * (int)sizeof(FitSlot<K>);
+                if (n > express_max_n<K>(lds_per_wave)) express_blocks = 0;
+                hipLaunchKernelGGL((k_cg_fit<P, Q, II, S, SPW>), dim3(grid_blocks + express_blocks),
+                                   dim3(64 * kFitWaves), 0, s, y, ld, n, N, init, init_status, coef_out, ll_out,
+                                   status_out, n_eval_out, n_grad_out, flags_out, ctl, xq, xready, grid_blocks,
+                                   join_express);
+                STS_CHECK_LAUNCH();
+                return ARIMA_OK;
             }
         });
     });
@@ -1503,25 +1348,22 @@ int launch_cg_fit_P(const double *y, int64_t ld, int n, int64_t N, int q, int I,
                     const int32_t *init_status, double *coef_out, double *ll_out, int32_t *status_out,
                     int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out, unsigned long long *ctl,
                     int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready, int join_express,
-                    int variant, const FitRounds *rounds, hipStream_t s) {
+                    hipStream_t s) {
     return with_smear(smear, [&](auto Sc) {
         return launch_cg_fit_PS<P, (decltype(Sc)::value != 0)>(y, ld, n, N, q, I, init, init_status, coef_out, ll_out,
                                                                status_out, n_eval_out, n_grad_out, flags_out, ctl,
                                                                grid_blocks, express_blocks, xq, xready, join_express,
-                                                               variant, rounds, s);
+                                                               s);
     });
 }
 
 // series one workgroup keeps in flight (blocks of the grid are sized from it)
 template <int P>
-int cg_fit_series_per_block_P(int q, int I, int variant) {
+int cg_fit_series_per_block_P(int q, int I) {
     return with_order(q, [&](auto Qc) {
         return with_bool(I, [&](auto Ic) {
             constexpr int Q = decltype(Qc)::value, II = decltype(Ic)::value;
             if constexpr (P + Q + II == 0) return 0;
-#if STS_REG_KERNEL
-            else if (variant == 3) return 64 + reg_lds_slots<P + Q + II>();
-#endif
             else return kFitWaves * fit_slots_per_wave<P + Q + II>();
         });
     });
@@ -1574,8 +1416,7 @@ int launch_model_flags_P(const double *coef, int64_t N, int q, int I, uint8_t *f
     EXT template int launch_cg_fit_PS<PP, SS>(const double *, int64_t, int, int64_t, int, int, const double *,    \
                                               const int32_t *, double *, double *, int32_t *, int32_t *,        \
                                               int32_t *, uint8_t *, unsigned long long *, int, int,             \
-                                              unsigned char *, unsigned *, int, int, const FitRounds *,         \
-                                              hipStream_t);
+                                              unsigned char *, unsigned *, int, hipStream_t);
 
 #define STS_DECLARE_P(PP, EXT)                                                                                  \
     STS_DECLARE_CG(PP, false, extern)                                                                           \
@@ -1587,8 +1428,8 @@ int launch_model_flags_P(const double *coef, int64_t N, int q, int I, uint8_t *f
     EXT template int launch_cg_fit_P<PP>(const double *, int64_t, int, int64_t, int, int, int, const double *,   \
                                          const int32_t *, double *, double *, int32_t *, int32_t *, int32_t *,  \
                                          uint8_t *, unsigned long long *, int, int, unsigned char *, unsigned *, \
-                                         int, int, const FitRounds *, hipStream_t);                             \
-    EXT template int cg_fit_series_per_block_P<PP>(int, int, int);                                                   \
+                                         int, hipStream_t);                                                     \
+    EXT template int cg_fit_series_per_block_P<PP>(int, int);                                                   \
     EXT template int launch_css_loglik_P<PP>(const double *, int64_t, int, int64_t, int, int, const double *,    \
                                              double *, hipStream_t);                                            \
     EXT template int launch_css_grad_P<PP>(const double *, int64_t, int, int64_t, int, int, int, const double *, \

@@ -32,30 +32,11 @@ int launch_hr_init(const double *y, int64_t ld, int n, int64_t N, int p, int q, 
 int launch_ar_fit(const double *y, int64_t ld, int n, int64_t N, int p, int I, double *coef_out, double *ll_out,
                   int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
                   hipStream_t s);
-// Workspaces of the rounds fit (variant 2, arima_fit_rounds.hpp), one set per fit in flight.
-constexpr int kRoundLists = 4;     // request lists per round: G, F with 2, 1, 0 predicted points
-constexpr int kRcStride = 8;       // round-control words per round (list counts, the pass kernel's tile counter)
-struct FitRounds {
-    unsigned char *rec;            // N x rounds_rec_bytes(k): the optimizer state of every series
-    double *resp;                  // N x rounds_resp_words(k): the response of its last pass
-    int32_t *lists;                // 2 x kRoundLists x N series ids (round parity)
-    int32_t *tail;                 // N: the series handed to k_cg_fit
-    uint8_t *mark;                 // N: the list of each series' next request (arima_fit_rounds.hpp)
-    unsigned *counts;              // rounds_ranges(N) x 8: per range of series, list counts, then offsets
-    unsigned *rc;                  // (max_rounds + 2) x kRcStride, zeroed before the fit; the tail count last
-    int max_rounds;                // rounds enqueued (the last one hands every unfinished series to k_cg_fit)
-    unsigned tail_at;              // a round with at most this many requests hands them to k_cg_fit
-    int pass_blocks, advance_blocks;   // persistent grids (single-wave workgroups)
-    int tail_express;              // 1: the tail runs on express waves only (a wave per series, rows in LDS)
-};
-int rounds_rec_bytes(int k);       // record stride of k parameters (a multiple of 128 B)
-int rounds_resp_words(int k);
-int64_t rounds_ranges(int64_t N);  // ranges of series the list compaction works on
 int launch_cg_fit(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, int smear,
                   const double *init, const int32_t *init_status, double *coef_out, double *ll_out,
                   int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
                   unsigned long long *ctl, int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready,
-                  int join_express, int variant, const FitRounds *rounds, hipStream_t s);
+                  int join_express, hipStream_t s);
 constexpr int kExpressRingEntries = 32768;      // k_cg_fit's express hand-offs per launch (entries never reused)
 constexpr int kExpressRingBytes = kExpressRingEntries * 512;   // x kExpressEntryBytes
 constexpr int kExpressReadyBytes = kExpressRingEntries * 4;
@@ -67,28 +48,15 @@ int launch_model_flags(const double *coef, int64_t N, int p, int q, int I, uint8
 // base_host: I + p + q host doubles (passed to the kernel by value)
 int launch_sample(double *out, int64_t ld, int64_t N, int T, int p, int d, int q, int I, const double *base_host,
                   double jitter, uint64_t seed, int64_t first, hipStream_t s);
-int cg_fit_series_per_block(int p, int q, int I, int variant);   // optimizer slots of one fit workgroup
+int cg_fit_series_per_block(int p, int q, int I);   // optimizer slots of one fit workgroup
 // k_cg_fit workgroups are single waves (4 per CU, one per SIMD, each with a quarter of the LDS): a wave that has
 // finished its series leaves the CU at once, so the next fit's waves take its SIMD and LDS share while the other
 // waves of the CU still run their slowest series (pipelined fits)
-#ifndef STS_FIT_BLOCK_WAVES
-#define STS_FIT_BLOCK_WAVES 1
-#endif
-constexpr int kFitBlockWaves = STS_FIT_BLOCK_WAVES;   // waves per k_cg_fit workgroup (1 or 4)
-#ifndef STS_FIT_WAVES_PER_CU
-#define STS_FIT_WAVES_PER_CU 4
-#endif
-constexpr int kFitWavesPerCU = STS_FIT_WAVES_PER_CU;  // resident k_cg_fit waves per CU (4: one per SIMD)
+constexpr int kFitBlockWaves = 1;            // waves per k_cg_fit workgroup
+constexpr int kFitWavesPerCU = 4;            // resident k_cg_fit waves per CU (one per SIMD)
 constexpr int kFitBlocksPerCU = kFitWavesPerCU / kFitBlockWaves;
 
-// fit_kernel = 3 (k_cg_fit_r, arima_fit_reg.hpp): two single-wave workgroups per SIMD, one optimizer slot per lane in
-// registers plus a reserve in the wave's eighth of the LDS. Its express waves stage rows of at most
-// cg_fit_reg_max_n(k) doubles; longer rows keep k_cg_fit (variant 0).
-constexpr int kRegWavesPerCU = 8;
-#ifndef STS_MERGE_LIVE_DEFAULT
-#define STS_MERGE_LIVE_DEFAULT 16            // k_cg_fit's drain merge threshold (option "merge_live"; 0 = off)
-#endif
-int cg_fit_reg_max_n(int k);
+constexpr int kMergeLiveDefault = 16;        // k_cg_fit's drain merge threshold (option "merge_live"; 0 = off)
 
 int hr_shape_status_host(int n, int p, int q, int I);
 int ar_shape_status_host(int n, int p, int I);

@@ -63,7 +63,6 @@ struct PendingStats {
 // Device workspace of one fit in flight: Hannan-Rissanen init, the fit kernel's counters and its express ring.
 struct FitWs {
     DevBuf init, hr_status, ctl, xring, xready;
-    DevBuf rec, resp, lists, tail, mark, counts, rc;   // the rounds fit (fit_kernel = 2): records, responses, lists
 };
 
 // One lane of the order search's concurrent fits (arima_order_search_batch*): its own stream, workspace and
@@ -109,7 +108,6 @@ struct FitCtx {
     unsigned long long *ctl_host = nullptr;   // pinned
     PendingStats pending;
     bool fit_ctl = false;                     // ctl_host holds (or will hold, in stream order) the kernel counters
-    bool rounds_last = false;                 // the context's last fit ran the rounds fit (fit_kernel 2)
     // host path (arima_fit_batch): device copies of one chunk and pinned staging of its input and outputs
     DevBuf d_series, d_coef, d_ll, d_status, d_neval, d_ngrad, d_flags, d_uinit;
     void *pin = nullptr;
@@ -133,25 +131,18 @@ struct arima_handle {
     int grid_blocks_override = 0;
     int express_blocks = -1;       // k_cg_fit express workgroups (-1: num_cus / 16)
     int express_ring = 0;          // express hand-offs per launch (0: the whole ring, sts::kExpressRingEntries)
-    int merge_live = STS_MERGE_LIVE_DEFAULT;
+    int merge_live = sts::kMergeLiveDefault;    // k_cg_fit drain merge: hand over at <= this many live slots (0: off)
     // express CUs of the order search's concurrent fits (-1: as "express_blocks"). 0 by default: with 16 lanes in
     // flight each fit's express workgroups held whole CUs for the fit's duration, mostly waiting (C5 262 144:
     // 14 728 series/s with them, 16 659 without; profiles/r04/g_merge)
     int search_express_blocks = 0;
     int donate_evals = 0;          // k_cg_fit: evaluations before a slot may go to an express wave (0: kernel default)
-    int donate_evals_drained = 0;  // ... once the batch's work counter has run out (0: kernel default)   // k_cg_fit drain merge: hand over at <= this many live slots (0: off)
+    int donate_evals_drained = 0;  // ... once the batch's work counter has run out (0: kernel default)
     // k_hr_init: 0 = a lane per series; > 0 = that many single-wave workgroups (grid-stride); -1 (default) = 1 024
     // for pipelined device fits (fit_pipeline > 1: C2 9.47-9.55 -> 9.68-9.75 M series/s, profiles/r04/m_hrgrid),
     // else 0 (alone it is 25.2 vs 26.9 ms at C2)
     int hr_grid = -1;
     int row_pad = 0;               // doubles (multiple of 16) added to the differenced rows' stride
-    int fit_kernel = 0;            // 0: k_cg_fit (LDS slots, 1 wave/SIMD); 2: rounds of streaming passes + k_cg_fit
-    int rounds_max = 96;           // rounds enqueued per fit (fit_kernel 2)
-    int64_t rounds_tail = -1;      // a round with at most this many requests hands them to k_cg_fit (-1: half its slots)
-    int rounds_pass_waves = 12;    // resident pass waves per CU the pass kernel's persistent grid assumes
-    int rounds_tail_express = 0;   // the rounds' tail on express waves only (1) or on k_cg_fit's bulk + express (0)
-    int rounds_tail_cus = 0;       // k_cg_fit grid of the rounds' tail: bulk CUs (0: all), express CUs (-1: default)
-    int rounds_tail_xcus = -1;
     int64_t last_express = 0;
     int64_t last_grid = 0;
     int search_lanes = 8;          // concurrent fits of the order search (2/4/8: 1269/1303/1408 series/s, profiles/r02/g_c5)
@@ -235,19 +226,26 @@ __global__ void k_fault_take(unsigned long long *__restrict__ rec) {
 
 // One grid point's fit into its search lane's counter sums (order-search stats, arima_get_last_stats): every kernel
 // counter word, and the fit's algorithmic flops by compute_stats' formula. cg = 0: the AR-only
-// shortcut or a uniform status (no counters; every series written).
+// shortcut or a uniform status (no counters; every series written). The fault words ctl[26..31] are not summed: the
+// lane keeps the first fault any of its fits recorded.
 __global__ void k_search_acc(const unsigned long long *__restrict__ ctl, unsigned long long *__restrict__ acc,
                              int64_t N, int n, int p, int q, int I, int cg) {
     if (threadIdx.x != 0) return;
-    for (int i = 0; i < kCtlWords; ++i) acc[i] += ctl[i];
+    for (int i = 0; i < kCtlWords; ++i)
+        if (i < 26 || i > 31) acc[i] += ctl[i];
+    if (acc[26] == 0 && ctl[26] != 0)
+        for (int i = 26; i <= 31; ++i) acc[i] = ctl[i];
     if (!cg) acc[32] += (unsigned long long)N;
     const int k = I + p + q, M = p > q ? p : q, m = M + 1;
     const double S = n - M > 0 ? n - M : 0;
     const double ff = 2.0 * (p + q) + 4, fg = ff + 2.0 * k * q + 1 + p + q + 2.0 * k;
     const double U = (double)(ctl[1] + ctl[18] + ctl[24] + ctl[7]), G = (double)(ctl[2] - ctl[18] + ctl[25]);
-    const double whr = (double)N * (3.0 * (n - m > 0 ? n - m : 0) * (m + 1) * (m + 1) +
-                                    3.0 * (n - 2 * M - 1 > 0 ? n - 2 * M - 1 : 0) * k * k +
-                                    2.0 * (n - m > 0 ? n - m : 0) * m);
+    // the AR-only shortcut (p > 0, q == 0) runs one OLS, not the Hannan-Rissanen init
+    const bool ar_only = p > 0 && q == 0;
+    const double whr = ar_only ? 0.0
+                               : (double)N * (3.0 * (n - m > 0 ? n - m : 0) * (m + 1) * (m + 1) +
+                                              3.0 * (n - 2 * M - 1 > 0 ? n - 2 * M - 1 : 0) * k * k +
+                                              2.0 * (n - m > 0 ? n - m : 0) * m);
     double *fl = reinterpret_cast<double *>(acc + kCtlWords);
     *fl = *fl + U * S * ff + G * S * fg + whr;
 }
@@ -405,7 +403,10 @@ int arima_get_last_stats(const arima_handle *hc, arima_fit_stats *out) {
         unsigned long long w[kCtlWords] = {};
         for (int j = 0; j < h->search_lanes_used; ++j) {
             const unsigned long long *a = h->search_acc_host + (size_t)j * (kCtlWords + 1);
-            for (int i = 0; i < kCtlWords; ++i) w[i] += a[i];
+            for (int i = 0; i < kCtlWords; ++i)
+                if (i < 26 || i > 31) w[i] += a[i];
+            if (w[26] == 0 && a[26] != 0)                    // the first lane's recorded fault
+                for (int i = 26; i <= 31; ++i) w[i] = a[i];
             double f;
             memcpy(&f, a + kCtlWords, sizeof f);
             flops += f;
@@ -432,6 +433,10 @@ int arima_get_last_stats(const arima_handle *hc, arima_fit_stats *out) {
         st.low_util_passes = (int64_t)w[37];
         st.merge_series = (int64_t)w[41];
         st.merge_waves = (int64_t)w[42];
+        st.fault = (int64_t)w[26];
+        for (int i = 0; i < 5; ++i) st.fault_info[i] = (int64_t)w[27 + i];
+        st.grid_blocks = h->last_grid;
+        st.express_blocks = h->last_express;
         st.flops = flops;
         float ms = 0;
         hipEventElapsedTime(&ms, h->ev[0], h->ev[3]);
@@ -458,19 +463,6 @@ static int check_fault(arima_handle *h, FitCtx &c) {
 
 static int take_fault(arima_handle *h);
 
-int arima_rounds_trace(arima_handle *h, unsigned *out, int max_words) {
-    if (!h || !out || max_words < 0) return ARIMA_E_INVALID_ARG;
-    std::lock_guard<std::mutex> lk(h->mu);
-    HIPCHK(h, hipSetDevice(h->device));
-    if (h->stats_ctx < 0) return 0;
-    FitCtx &c = h->fctx[h->stats_ctx];
-    if (c.has_done) HIPCHK(h, hipEventSynchronize(c.ev_done));
-    if (!c.ws.rc.ptr || !c.rounds_last) return 0;     // no rounds words of the context's last fit
-    const int words = (int)std::min<size_t>((size_t)max_words, c.ws.rc.bytes / sizeof(unsigned));
-    HIPCHK(h, hipMemcpy(out, c.ws.rc.ptr, (size_t)words * sizeof(unsigned), hipMemcpyDeviceToHost));
-    return words;
-}
-
 int arima_synchronize(arima_handle *h) {
     if (!h) return ARIMA_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
@@ -494,22 +486,6 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
     if (!h || !name) return ARIMA_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
     if (!strcmp(name, "smear")) { h->smear = value ? 1 : 0; return ARIMA_OK; }
-    if (!strcmp(name, "fit_kernel")) {
-        if (value != 0 && value != 2 && value != 3) return set_err(h, ARIMA_E_INVALID_ARG, "fit_kernel: 0, 2 or 3");
-        if (value == 3 && sts::cg_fit_reg_max_n(1) < 0)
-            return set_err(h, ARIMA_E_UNSUPPORTED, "fit_kernel 3: built only with -DSTS_REG_KERNEL=1");
-        h->fit_kernel = (int)value;
-        return ARIMA_OK;
-    }
-    if (!strcmp(name, "rounds_max")) { h->rounds_max = (int)std::min<int64_t>(4096, std::max<int64_t>(1, value)); return ARIMA_OK; }
-    if (!strcmp(name, "rounds_tail_express")) { h->rounds_tail_express = value ? 1 : 0; return ARIMA_OK; }
-    if (!strcmp(name, "rounds_tail_cus")) { h->rounds_tail_cus = (int)std::max<int64_t>(0, value); return ARIMA_OK; }
-    if (!strcmp(name, "rounds_tail_xcus")) { h->rounds_tail_xcus = (int)std::max<int64_t>(-1, value); return ARIMA_OK; }
-    if (!strcmp(name, "rounds_tail")) { h->rounds_tail = std::max<int64_t>(-1, value); return ARIMA_OK; }
-    if (!strcmp(name, "rounds_pass_waves")) {
-        h->rounds_pass_waves = (int)std::min<int64_t>(32, std::max<int64_t>(1, value));
-        return ARIMA_OK;
-    }
     if (!strcmp(name, "row_pad")) {                 // doubles, rounded up to whole 128-B lines
         h->row_pad = (int)round_up(std::min<int64_t>(4096, std::max<int64_t>(0, value)), 16);
         return ARIMA_OK;
@@ -556,10 +532,7 @@ int arima_get_option(const arima_handle *hc, const char *name, int64_t *value) {
         {"smear", h->smear}, {"express_blocks", h->express_blocks}, {"grid_blocks", h->grid_blocks_override},
         {"search_lanes", h->search_lanes}, {"fit_pipeline", h->pipeline}, {"host_pipeline", h->host_pipeline},
         {"host_chunk", h->host_chunk}, {"fit_slice_bytes", h->fit_slice_bytes}, {"express_ring", h->express_ring},
-        {"fit_kernel", h->fit_kernel}, {"hr_grid", h->hr_grid}, {"row_pad", h->row_pad}, {"rounds_max", h->rounds_max},
-        {"rounds_tail", h->rounds_tail}, {"rounds_pass_waves", h->rounds_pass_waves},
-        {"rounds_tail_express", h->rounds_tail_express}, {"rounds_tail_cus", h->rounds_tail_cus},
-        {"rounds_tail_xcus", h->rounds_tail_xcus}, {"merge_live", h->merge_live},
+        {"hr_grid", h->hr_grid}, {"row_pad", h->row_pad}, {"merge_live", h->merge_live},
         {"search_express_blocks", h->search_express_blocks}, {"donate_evals", h->donate_evals},
         {"donate_evals_drained", h->donate_evals_drained}};
     for (const auto &o : opts)
@@ -596,19 +569,6 @@ static hipError_t end_fit(FitCtx &c, hipStream_t s) {
     hipError_t e = hipEventRecord(c.ev_done, s);
     if (e == hipSuccess) c.has_done = true;
     return e;
-}
-
-// Workspaces of the rounds fit (fit_kernel = 2) for N series of k parameters.
-static int ensure_rounds_ws(arima_handle *h, FitWs &ws, int64_t N, int k) {
-    const int kk = std::max(1, std::min(k, 11));
-    int rc = ws.rec.ensure((size_t)N * sts::rounds_rec_bytes(kk));
-    if (rc == ARIMA_OK) rc = ws.resp.ensure((size_t)N * sts::rounds_resp_words(kk) * sizeof(double));
-    if (rc == ARIMA_OK) rc = ws.lists.ensure((size_t)2 * sts::kRoundLists * N * sizeof(int32_t));
-    if (rc == ARIMA_OK) rc = ws.tail.ensure((size_t)N * sizeof(int32_t));
-    if (rc == ARIMA_OK) rc = ws.mark.ensure((size_t)N);
-    if (rc == ARIMA_OK) rc = ws.counts.ensure((size_t)sts::rounds_ranges(N) * 8 * sizeof(unsigned));
-    if (rc == ARIMA_OK) rc = ws.rc.ensure((size_t)(h->rounds_max + 2) * sts::kRcStride * sizeof(unsigned));
-    return rc;
 }
 
 // Hannan-Rissanen init (unless user init) and the fit kernel -- or the AR-only shortcut, or a uniform per-series
@@ -671,12 +631,10 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
     if (xcus >= cus) xcus = cus - 1;
     int bcus = h->grid_blocks_override;
     if (bcus <= 0) bcus = std::max(1, cus - xcus);
-    // fit_kernel 3 (two waves per SIMD) where its express waves can stage the rows, else k_cg_fit
-    const int variant = (h->fit_kernel == 3 && n > sts::cg_fit_reg_max_n(k)) ? 0 : h->fit_kernel;
-    const int bpc = variant == 3 ? sts::kRegWavesPerCU : sts::kFitBlocksPerCU;
+    const int bpc = sts::kFitBlocksPerCU;
     int xblocks = xcus * bpc;
     int blocks = bcus * bpc;
-    const int per_block = std::max(1, sts::cg_fit_series_per_block(p, q, I, variant));
+    const int per_block = std::max(1, sts::cg_fit_series_per_block(p, q, I));
     const int64_t need = (N + per_block - 1) / per_block;
     if (blocks > need) blocks = (int)need;
     if (xblocks > 0 || h->merge_live > 0) {                   // the merge pool: the ring's upper 3/4
@@ -684,35 +642,11 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
         RCCHK(h, ws.xready.ensure(sts::kExpressReadyBytes), "workspace");
         HIPCHK(h, hipMemsetAsync(ws.xready.ptr, 0, sts::kExpressReadyBytes, s));
     }
-    sts::FitRounds rounds{};
-    if (variant == 2) {
-        RCCHK(h, ensure_rounds_ws(h, ws, N, k), "workspace");
-        HIPCHK(h, hipMemsetAsync(ws.rc.ptr, 0, (size_t)(h->rounds_max + 2) * sts::kRcStride * sizeof(unsigned), s));
-        rounds.rec = ws.rec.as<unsigned char>();
-        rounds.resp = ws.resp.as<double>();
-        rounds.lists = ws.lists.as<int32_t>();
-        rounds.tail = ws.tail.as<int32_t>();
-        rounds.mark = ws.mark.as<uint8_t>();
-        rounds.counts = ws.counts.as<unsigned>();
-        rounds.rc = ws.rc.as<unsigned>();
-        rounds.max_rounds = h->rounds_max;
-        rounds.tail_at = (unsigned)std::min<int64_t>(
-            0xffffffffll, h->rounds_tail >= 0 ? h->rounds_tail : (int64_t)blocks * per_block / 2);
-        rounds.pass_blocks = cus * h->rounds_pass_waves;
-        rounds.advance_blocks = cus * 8;
-        rounds.tail_express = h->rounds_tail_express;
-        // the tail's size is known on the device only: a grid of rounds_tail_cus CUs' worth of bulk workgroups
-        // (<= 0: all), rounds_tail_xcus of express ones (< 0: as a plain fit)
-        blocks = (h->rounds_tail_cus > 0 ? std::min(bcus, h->rounds_tail_cus) : bcus) * bpc;
-        if (h->rounds_tail_xcus >= 0) xblocks = std::min(h->rounds_tail_xcus, cus) * bpc;
-        if (blocks + xblocks == 0) blocks = bpc;
-    }
     *grid_out = blocks;
     *express_out = xcus;                    // in CUs, the unit of the "express_blocks" option
     RCCHK(h, sts::launch_cg_fit(y, ldn, n, N, p, q, I, h->smear, init, init_status, d_coef, d_ll, d_status, d_neval,
                                 d_ngrad, d_flags, ws.ctl.as<unsigned long long>(), blocks, xblocks,
-                                ws.xring.as<unsigned char>(), ws.xready.as<unsigned>(), shared_gpu ? 0 : 1, variant,
-                                &rounds, s),
+                                ws.xring.as<unsigned char>(), ws.xready.as<unsigned>(), shared_gpu ? 0 : 1, s),
           "cg_fit");
     hipLaunchKernelGGL(k_fault_merge, dim3(1), dim3(64), 0, s, ws.ctl.as<unsigned long long>(),
                        h->dev_fault.as<unsigned long long>());
@@ -731,7 +665,6 @@ static int reserve_fit_ws(arima_handle *h, int count, int64_t N, int64_t ldn, in
         RCCHK(h, c.ws.ctl.ensure(kCtlWords * sizeof(unsigned long long)), "workspace");
         RCCHK(h, c.ws.xring.ensure(sts::kExpressRingBytes), "workspace");
         RCCHK(h, c.ws.xready.ensure(sts::kExpressReadyBytes), "workspace");
-        if (h->fit_kernel == 2) RCCHK(h, ensure_rounds_ws(h, c.ws, N, k), "workspace");
     }
     return ARIMA_OK;
 }
@@ -754,7 +687,6 @@ static int fit_device_locked(arima_handle *h, FitCtx &c, int ci, int reserve, co
     const int n = std::max(T - d, 0);
     const int64_t ldn = row_stride(h, n);
     c.pending = PendingStats{};
-    c.rounds_last = false;
     if (slot < 0) {
         h->stats = arima_fit_stats{};
         h->stats_ctx = ci;
@@ -786,7 +718,6 @@ static int fit_device_locked(arima_handle *h, FitCtx &c, int ci, int reserve, co
     ps.ar_only = p > 0 && q == 0;
     ps.user_init = d_user_init != nullptr;
     ps.cg = !ps.ar_only && method == ARIMA_METHOD_CSS_CGD && k > 0;
-    c.rounds_last = ps.cg && h->fit_kernel == 2;
     ps.grid = grid;
     ps.express = xblocks;
     ps.valid = true;
@@ -1374,7 +1305,6 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
         if (rc == ARIMA_OK) rc = ln.acc.ensure((kCtlWords + 1) * sizeof(unsigned long long));
         if (rc == ARIMA_OK) rc = ln.ws.xring.ensure(sts::kExpressRingBytes);
         if (rc == ARIMA_OK) rc = ln.ws.xready.ensure(sts::kExpressReadyBytes);
-        if (rc == ARIMA_OK && h->fit_kernel == 2) rc = ensure_rounds_ws(h, ln.ws, N, 11);
         if (rc != ARIMA_OK) {
             if (j == 0) return set_err(h, rc, "order search workspace");
             break;                                 // fewer lanes instead of failing the call
@@ -1458,6 +1388,10 @@ static int order_search_locked(arima_handle *h, const double *d_series, int64_t 
                                      ln.coef.as<double>(), ln.ll.as<double>(), ln.status.as<int32_t>(),
                                      ln.neval.as<int32_t>(), ln.ngrad.as<int32_t>(), ln.flags.as<uint8_t>(), ln.stream,
                                      nullptr, &gridb, &xb, L > 1, L > 1 ? h->search_express_blocks : -2, true), "fit");
+                if (gridb > 0) {
+                    h->last_grid = gridb;
+                    h->last_express = xb;
+                }
                 hipLaunchKernelGGL(k_search_acc, dim3(1), dim3(64), 0, ln.stream, ln.ws.ctl.as<unsigned long long>(),
                                    ln.acc.as<unsigned long long>(), N, n, p, q, I,
                                    (p > 0 && q == 0) || method != ARIMA_METHOD_CSS_CGD || I + p + q == 0 ? 0 : 1);

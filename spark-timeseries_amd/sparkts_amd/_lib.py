@@ -48,7 +48,7 @@ EXPORTED = [
     "arima_difference_batch", "arima_inverse_difference_batch", "arima_css_loglik_batch",
     "arima_css_gradient_batch", "arima_hannan_rissanen_batch", "arima_forecast_batch", "arima_model_flags_batch",
     "arima_sample_batch_device", "arima_order_search_batch", "arima_order_search_batch_device",
-    "arima_forecast_batch_device", "arima_synchronize", "arima_rounds_trace",
+    "arima_forecast_batch_device", "arima_synchronize",
 ]
 
 
@@ -122,7 +122,6 @@ def load():
         L.arima_get_last_stats.argtypes = [H, ctypes.POINTER(FitStats)]
         L.arima_set_option.argtypes = [H, ctypes.c_char_p, _i64]
         L.arima_get_option.argtypes = [H, ctypes.c_char_p, ctypes.POINTER(_i64)]
-        L.arima_rounds_trace.argtypes = [H, ctypes.POINTER(ctypes.c_uint), ctypes.c_int]
         L.arima_synchronize.argtypes = [H]
         L.arima_fit_batch.argtypes = [H, _dp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _dp, _dp, _dp, _i32p,
                                       _i32p, _i32p, _u8p]
@@ -163,10 +162,8 @@ class Engine:
             raise EngineError(f"arima_create(device={device}) failed with {rc}: no usable HIP device")
         self.h = h
         self.device = device
-        # engine-wide knobs from the environment (A/B runs of the test suite and the bench): SPARKTS_FIT_KERNEL=0|2
-        if os.environ.get("SPARKTS_FIT_KERNEL", "") != "":
-            self.set_option("fit_kernel", int(os.environ["SPARKTS_FIT_KERNEL"]))
-        # any option: SPARKTS_OPTIONS="hr_grid=1024,fit_pipeline=2"
+        # engine-wide knobs from the environment (A/B runs of the test suite and the bench), any option:
+        # SPARKTS_OPTIONS="hr_grid=1024,fit_pipeline=2"
         for kv in filter(None, os.environ.get("SPARKTS_OPTIONS", "").split(",")):
             name, _, val = kv.partition("=")
             self.set_option(name.strip(), int(val))
@@ -195,19 +192,6 @@ class Engine:
         v = _i64()
         self._check(self.L.arima_get_option(self.h, name.encode(), ctypes.byref(v)), "arima_get_option")
         return int(v.value)
-
-    def rounds_trace(self):
-        """Round-control words of the last device fit (fit_kernel 2): an array (rounds, 8) -- counts of lists G,
-        F+2, F+1, F+0, the tile counter -- and the tail count."""
-        R = self.get_option("rounds_max")
-        buf = (ctypes.c_uint * ((R + 2) * 8))()
-        n = self.L.arima_rounds_trace(self.h, buf, (R + 2) * 8)
-        if n < 0:
-            self._check(n, "arima_rounds_trace")
-        a = np.frombuffer(buf, dtype=np.uint32)[:n].copy()
-        if a.size < (R + 2) * 8:
-            return None, None
-        return a[: R * 8].reshape(R, 8), int(a[(R + 1) * 8])
 
     def synchronize(self):
         """Wait for the device work of every call issued on this handle (the *_device calls are asynchronous)."""

@@ -747,91 +747,3 @@ def test_row_pad_is_transparent(engine):
         assert _same(x, y)
     for x, y in zip(qa, qb):
         assert _same(np.asarray(x), np.asarray(y))
-
-
-ROUNDS_CONFIGS = {
-    # every series through the rounds (hand-off only in the last round, past every fit's end)
-    "all_rounds": dict(rounds_max=400, rounds_tail=0),
-    # the last round hands every unfinished series to k_cg_fit (bulk + express), which resumes from the records
-    "last_round_handoff": dict(rounds_max=12, rounds_tail=0),
-    # hand-off by count: a round with <= 1000 requests goes to k_cg_fit
-    "count_handoff": dict(rounds_max=400, rounds_tail=1000),
-    # hand-off to express waves only (a wave per series, direct claims from the tail list)
-    "express_tail": dict(rounds_max=10, rounds_tail=0, rounds_tail_express=1),
-}
-
-
-def _with_options(engine, opts, fn):
-    old = {k: engine.get_option(k) for k in opts}
-    old["fit_kernel"] = engine.get_option("fit_kernel")
-    try:
-        engine.set_option("fit_kernel", 2)
-        for k, v in opts.items():
-            engine.set_option(k, v)
-        return fn()
-    finally:
-        for k, v in old.items():
-            engine.set_option(k, v)
-
-
-@pytest.mark.parametrize("cfg", sorted(ROUNDS_CONFIGS))
-def test_rounds_fit_c2_batch(engine, cfg):
-    # fit_kernel 2 (arima_fit_rounds.hpp): rounds of streaming passes + the k_cg_fit tail, bit-identical to the oracle
-    N, T = 2048, 1024
-    s = _device_sample(engine, N, T, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 4242).cpu().numpy()
-    res, st_g = _with_options(engine, ROUNDS_CONFIGS[cfg], lambda: (engine.fit_batch(s, 2, 1, 2, True), engine.stats()))
-    st, coef, ll, cnt = O.fit_batch(s, 2, 1, 2, 1)
-    exp = dict(status=st, coef=coef, ll=ll, n_eval=cnt[:, 0], n_grad=cnt[:, 1],
-               flags=np.array([O.model_flags(coef[i], 2, 2, 1) if st[i] == 0 else 0 for i in range(N)]))
-    check_fit(res, exp, f"rounds_{cfg}")
-    assert st_g["series_done"] == N and st_g["fault"] == 0
-    assert st_g["n_eval"] == int(cnt[:, 0].sum())
-
-
-@pytest.mark.parametrize("name", ["c1_101_T500", "c2_212_T1024_shift", "c4_515_T512", "kat_ds1_101_userinit",
-                                  "edge_T12_212", "edge_nan_101", "edge_userinit_nonfinite", "grid_p0d1q3i0",
-                                  "grid_p3d2q5i1", "kat_mt10_112_noint"])
-@pytest.mark.parametrize("cfg", ["all_rounds", "last_round_handoff"])
-def test_rounds_fit_golden(engine, name, cfg):
-    meta, arr = load_case(name)
-    opts = dict(ROUNDS_CONFIGS[cfg], smear=meta["smear"])
-    res = _with_options(engine, opts, lambda: engine.fit_batch(arr["series"], meta["p"], meta["d"], meta["q"], meta["I"],
-                                                               meta["method"], arr.get("user_init")))
-    check_fit(res, arr, f"{name}/{cfg}")
-
-
-def test_rounds_fit_c4_T4096(engine):
-    # C4 rows (T = 4096) do not fit an express wave: the tail resumes on k_cg_fit's bulk waves
-    N, T = 48, 4096
-    base = [0.1, 0.4, -0.2, 0.1, 0.05, -0.05, 0.3, 0.2, -0.1, 0.05, 0.05]
-    s = _device_sample(engine, N, T, 5, 1, 5, 1, base, 0.02, 20261015).cpu().numpy()
-    res = _with_options(engine, ROUNDS_CONFIGS["last_round_handoff"], lambda: engine.fit_batch(s, 5, 1, 5, True))
-    st, coef, ll, cnt = O.fit_batch(s, 5, 1, 5, 1)
-    exp = dict(status=st, coef=coef, ll=ll, n_eval=cnt[:, 0], n_grad=cnt[:, 1],
-               flags=np.array([O.model_flags(coef[i], 5, 5, 1) if st[i] == 0 else 0 for i in range(N)]))
-    check_fit(res, exp, "rounds_c4_T4096")
-
-
-def test_rounds_trace_accounts_for_every_request(engine):
-    # the round-control words: per round, the listed requests equal the lane passes the kernels counted
-    import torch
-    N, T, k = 4096, 1024, 5
-    s = _device_sample(engine, N, T, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 99)
-    o = {n: torch.empty(N * (k if n == "coef" else 1), dtype=t, device="cuda")
-         for n, t in [("coef", torch.float64), ("ll", torch.float64), ("status", torch.int32), ("n_eval", torch.int32),
-                      ("n_grad", torch.int32), ("flags", torch.uint8)]}
-
-    def run():                                 # the device entry point: the trace reads that fit's context
-        engine.fit_batch_device(s.data_ptr(), N, T, T, 2, 1, 2, 1, o["coef"].data_ptr(), o["ll"].data_ptr(),
-                                o["status"].data_ptr(), o["n_eval"].data_ptr(), o["n_grad"].data_ptr(),
-                                o["flags"].data_ptr(), blocking=True)
-        return engine.stats(), engine.rounds_trace()
-    st_g, (rc, tail) = _with_options(engine, dict(rounds_max=40, rounds_tail=0), run)
-    assert rc is not None and rc.shape == (40, 8)
-    active = rc[:, :4].sum(axis=1).astype(np.int64)
-    assert active[0] == N and rc[0, 0] == N                 # round 0: a G request for every series
-    assert np.all(np.diff(active) <= 0)                     # a series leaves the rounds only when it is done
-    assert 0 <= tail <= active[-1]                          # the last round hands its unfinished series over
-    # every listed request ran one lane pass; the tail kernel ran the others
-    assert int(active.sum()) <= st_g["f_passes"] + st_g["g_passes"] + st_g["express_f_passes"] + st_g["express_g_passes"]
-    assert st_g["series_done"] == N

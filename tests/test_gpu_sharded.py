@@ -50,3 +50,22 @@ def test_two_ranks_on_one_gpu_match_single_rank(tmp_path):
         assert a.shape == b.shape, k
         assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), k
     assert (one["status"] == 0).mean() > 0.99
+
+
+def test_bench_two_ranks_on_one_gpu_checks_every_rank_against_the_oracle():
+    # the multi-GPU bench line is self-checking -- every rank compares the first rows of its own
+    # shard with the oracle and the verdicts meet in gloo reductions (here: 2 ranks sharing GPU 0)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "0", "--series", "16384",
+           "--steps", "2", "--warmup", "1", "--e2e", "0", "--cpu-seconds", "2", "--pipeline", "2"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    par = line["parity"]
+    assert line["n_gpus"] == 2 and par["ranks_checked"] == 2
+    assert par["oracle_rows"] >= 2 * 256 and par["bit_identical"] == par["oracle_rows"]
+    assert par["every_rank_bit_identical"] and par["min_rank_fraction"] == 1.0 and par["vs_isolated"]
+    assert line["cpu_baseline"] is None                     # the CPU baseline is timed at N = 1 only

@@ -31,21 +31,31 @@ WORKER = r"""
 import os, sys, numpy as np, torch.distributed as dist
 sys.path[:0] = [os.environ["ROOT"], os.path.join(os.environ["ROOT"], "spark-timeseries_amd"),
                 os.path.join(os.environ["ROOT"], "oracle")]
-from sparkts_amd.sharding import shard_range, max_over_ranks, gather_results
+from sparkts_amd.sharding import shard_range, max_over_ranks, gather_results, parity_over_ranks
 import oracle as O
 dist.init_process_group("gloo")
 rank, world = dist.get_rank(), dist.get_world_size()
 rng = np.random.default_rng(0)
-N, T = 24, 200
+N, T = 25, 200
 allser = np.stack([O.add_time_dependent_effects(rng.standard_normal(T), 1, 0, 1, 1, [1.0, 0.4, 0.3]) for _ in range(N)])
 b, e = shard_range(N, rank, world)
 st, coef, ll, cnt = O.fit_batch(allser[b:e], 1, 0, 1, 1)
 t = max_over_ranks(float(rank + 1), dist)
-st_all, coef_all = gather_results([st, coef], dist)
+st_all, coef_all, cnt_all = gather_results([st, coef, cnt], dist)
+# bench.py's per-rank oracle parity: every rank checks its own rows, the verdicts meet in gloo sum / min reductions
+st_b, coef_b, _, cnt_b = O.fit_batch(allser[b:e], 1, 0, 1, 1)
+ok = int(((st_b == st) & (coef_b.view(np.int64) == coef.view(np.int64)).all(axis=1)).sum())
+par = parity_over_ranks(ok, e - b, dist)
+bad = parity_over_ranks(ok - (1 if rank == 1 else 0), e - b, dist)     # one rank reports a mismatching row
 if rank == 0:
-    st1, coef1, _, _ = O.fit_batch(allser, 1, 0, 1, 1)
+    st1, coef1, _, cnt1 = O.fit_batch(allser, 1, 0, 1, 1)
     assert t == float(world), t
-    assert np.array_equal(st_all, st1) and np.array_equal(coef_all, coef1)
+    assert np.array_equal(st_all, st1) and np.array_equal(coef_all, coef1) and np.array_equal(cnt_all, cnt1)
+    assert coef_all.shape == (N, 3) and cnt_all.dtype == cnt1.dtype
+    assert par == {"ranks": world, "oracle_rows": N, "bit_identical": N, "min_rank_fraction": 1.0,
+                   "every_rank_bit_identical": True}, par
+    assert bad["ranks"] == world and bad["bit_identical"] == N - 1 and not bad["every_rank_bit_identical"]
+    assert bad["min_rank_fraction"] < 1.0
     print("MULTIRANK_OK", flush=True)
 dist.barrier()
 dist.destroy_process_group()
