@@ -14,6 +14,8 @@
  *   - ARIMAModel.gradientlogLikelihoodCSSARMA                                   (ARIMA.scala:465-534)
  *   - ARIMA.fitWithCSSCGD + ARIMA.fitModel dispatch                             (ARIMA.scala:79-116,174-200)
  *   - ARIMAModel.forecast / addTimeDependentEffects / removeTimeDependentEffects (ARIMA.scala:629-764)
+ *   - TimeSeriesStatisticalTests.kpsstest + neweyWestVarianceEstimator (stats/TimeSeriesStatisticalTests.scala:369-431),
+ *     the differencing-order test of ARIMA.autoFit (the stepwise walk itself is restated in oracle.py: autofit)
  *   - third-party algorithms the path calls, which are NOT vendored in the reference:
  *       commons-math3 3.4.1 (pom.xml:466-470): NonLinearConjugateGradientOptimizer (FLETCHER_REEVES),
  *       LineSearch, BracketFinder, BrentOptimizer, SimpleValueChecker, SimpleUnivariateValueChecker,
@@ -354,6 +356,54 @@ int orc_hannan_rissanen(const double *y, int n, int p, int q, int I, double *par
     st = orc_ols(yTrunc + M, X, rows, ncx, I, params);        /* :237-240, noIntercept = !includeIntercept */
     free(X); free(errors);
     return st;
+}
+
+/* ===================================================================================================== */
+/* TimeSeriesStatisticalTests.kpsstest  stats/TimeSeriesStatisticalTests.scala:369-431 (used by ARIMA.autoFit)   */
+/* ===================================================================================================== */
+
+/* method 0 = "c" (regressors: a column of ones), 1 = "ct" (ones and the time trend 1..n), both fitted by
+ * OLSMultipleLinearRegression with setNoIntercept(true) (:375-385). Writes the statistic; returns ARIMA_ST_*
+ * (the OLS shape checks throw for n <= number of regressors). */
+int orc_kpss(const double *ts, int n, int method, double *stat_out) {
+    const int ncx = method == 1 ? 2 : 1;
+    double *X = (double *)calloc((size_t)(n > 0 ? n : 1) * 2, sizeof(double));
+    for (int r = 0; r < n; r++) {
+        X[(size_t)r * ncx] = 1.0;                                   /* Array.fill(n)(1.0)                  :374 */
+        if (ncx == 2) X[(size_t)r * ncx + 1] = 1.0 + (double)r;     /* Array.tabulate(n)(x => 1.0 + x)     :379 */
+    }
+    double beta[2];
+    int st = orc_ols(ts, X, n, ncx, 0, beta);
+    if (st != ARIMA_ST_OK) { free(X); return st; }
+    /* estimateResiduals: y - X.operate(b) (Array2DRowRealMatrix.operate: sum = 0; sum += x_rj * b_j)      :384 */
+    double *e = (double *)malloc(sizeof(double) * (size_t)n);
+    for (int r = 0; r < n; r++) {
+        double sum = 0.0;
+        for (int j = 0; j < ncx; j++) sum = sum + X[(size_t)r * ncx + j] * beta[j];
+        e[r] = ts[r] - sum;
+    }
+    free(X);
+    /* s2 = residuals.scanLeft(0.0)(_ + _).tail.map(math.pow(_, 2)).sum (left folds; pow(x, 2) = x * x)   :386 */
+    double cum = 0.0, s2 = 0.0;
+    for (int r = 0; r < n; r++) { cum = cum + e[r]; s2 = s2 + cum * cum; }
+    /* lag = (3 * math.sqrt(n) / 13).toInt                                                                 :390 */
+    const int lag = (int)(3.0 * sqrt((double)n) / 13.0);
+    /* neweyWestVarianceEstimator(residuals, lag)                                                        :405-431 */
+    double sumOfTerms = 0.0;
+    for (int i = 1; i <= lag; i++) {
+        double cell = 0.0;
+        for (int j = i; j < n; j++) cell = cell + e[j] * e[j - i];
+        sumOfTerms = sumOfTerms + cell * (1.0 - ((double)i / (double)(lag + 1)));
+    }
+    const double partial = (sumOfTerms * 2.0) / (double)n;
+    double sq = 0.0;
+    for (int r = 0; r < n; r++) sq = sq + e[r] * e[r];
+    const double lrv = partial + sq / (double)n;
+    free(e);
+    /* (s2 / longRunVariance) / (n * n): n * n is an Int product (32-bit)                                   :392 */
+    const int32_t nn = (int32_t)((uint32_t)n * (uint32_t)n);
+    *stat_out = (s2 / lrv) / (double)nn;
+    return ARIMA_ST_OK;
 }
 
 /* ===================================================================================================== */

@@ -69,6 +69,8 @@ def lib():
                                                         ctypes.c_int, ctypes.c_int, _dp, _dp]
         L.orc_lag_matrix.restype = ctypes.c_int
         L.orc_lag_matrix.argtypes = [_dp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _dp]
+        L.orc_kpss.restype = ctypes.c_int
+        L.orc_kpss.argtypes = [_dp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
         L.orc_set_threads.restype = None
         L.orc_set_threads.argtypes = [ctypes.c_int]
         _lib = L
@@ -288,3 +290,102 @@ def order_search(series, max_p=5, max_d=2, max_q=5, intercept_mode=2, method=0, 
                             coef_best[i] = 0.0
                             coef_best[i, :k] = coef[i, :k]
     return order, coef_best, aic_best
+
+
+# ---- ARIMA.autoFit (ARIMA.scala:280-375) -----------------------------------------------------------------------
+KPSS_CRITICAL = {0: {0.10: 0.347, 0.05: 0.463, 0.025: 0.574, 0.01: 0.739},      # "c"   (TimeSeriesStatisticalTests.scala:338-340)
+                 1: {0.10: 0.119, 0.05: 0.146, 0.025: 0.176, 0.01: 0.216}}      # "ct"  (:349-351)
+
+# autoFit outcomes beyond fitModel's (include/sparkts_arima.h)
+ST_NOT_STATIONARY = 11      # "stationarity not achieved with differencing order <= maxD" (ARIMA.scala:293-296)
+ST_NO_MODEL = 12            # no candidate qualified: curBestModel stays null (ARIMA.scala:322, :304 -> NPE)
+ST_CGD_FALLBACK = 13        # a css-cgd candidate failed in the optimizer where the reference tries css-bobyqa
+                            # (ARIMA.scala:315-319); the selection treats that fallback as failed too
+CGD_FALLBACK_STATUSES = (1, 2, 3, 7)   # MaxEval, BracketFinder cap, MaxIter, SearchInterval: thrown by the optimizer
+
+
+def kpss(ts, method="c"):
+    """TimeSeriesStatisticalTests.kpsstest (stats/TimeSeriesStatisticalTests.scala:369-393): (status, statistic)."""
+    ts, pt = _c(ts)
+    stat = ctypes.c_double(float("nan"))
+    st = lib().orc_kpss(pt, len(ts), 1 if method == "ct" else 0, ctypes.byref(stat))
+    return st, stat.value
+
+
+def autofit_select_d(ts, max_d):
+    """autoFit's choice of d (ARIMA.scala:287-297): the first d in 0..max_d whose differencesOfOrderD(ts, d) -- NOT
+    dropped -- passes kpsstest(_, "c") at 5 %. Returns (status, d): status != 0 when kpsstest throws (n <= 1) or no
+    d passes (ST_NOT_STATIONARY)."""
+    for d in range(max_d + 1):
+        st, stat = kpss(differences_of_order_d(ts, d), "c")
+        if st != 0:
+            return st, -1
+        if stat < KPSS_CRITICAL[0][0.05]:
+            return 0, d
+    return ST_NOT_STATIONARY, -1
+
+
+def autofit(ts, max_p=5, max_d=2, max_q=5, smear=DEFAULT_SMEAR, trace=None):
+    """ARIMA.autoFit (ARIMA.scala:280-304) + findBestARMAModel (:310-375), restated with its quirks:
+    - the ARMA fits run on differencesOfOrderD(ts, d) WITHOUT .drop(d) (:298): the first d raw values stay in;
+    - the intercept is used only if d <= 1 (:300);
+    - the first candidates (0,0), (2,2), (1,0), (0,1) are not bounds-checked (:325-327);
+    - the neighbourhood varies p and flips the intercept but never q (`curBestModel.q`, :364);
+    - a candidate counts if its fit returned normally, it is stationary and invertible (:342) and its approxAIC
+      (-2 * logLikelihoodCSS + 2 * (p + q + c), :826-830) is strictly below the incumbent's (starting at
+      Double.MaxValue, :323); the new incumbent is the first minimum in candidate order (minBy, :350).
+    fitTryBothStrategies (:315-319) falls back to css-bobyqa when css-cgd throws; BOBYQA is not restated, so such a
+    candidate is treated as failed and the result carries ST_CGD_FALLBACK.
+    Returns dict(status, order (p, d, q, intercept), coef (11, zero-padded), aic, n_fits)."""
+    ts = np.ascontiguousarray(ts, dtype=np.float64)
+    out = dict(status=0, order=(-1, -1, -1, -1), coef=np.full(11, np.nan), aic=float("inf"), n_fits=0)
+    st, d = autofit_select_d(ts, max_d)
+    if st != 0:
+        out["status"] = st
+        return out
+    diffed = differences_of_order_d(ts, d)
+    start_i = 1 if d <= 1 else 0
+    best_aic = 1.7976931348623157e308
+    best = None
+    fallback = False
+    past = set()
+    nxt = [(0, 0, start_i), (2, 2, start_i), (1, 0, start_i), (0, 1, start_i)]
+    cache = {}
+    while True:
+        past.update(nxt)
+        improving = []
+        for (p, q, I) in nxt:
+            if (p, q, I) not in cache:
+                r = fit(diffed, p, 0, q, I, smear=smear)
+                out["n_fits"] += 1
+                cache[(p, q, I)] = r
+                if r["status"] in CGD_FALLBACK_STATUSES and not (p > 0 and q == 0):
+                    fallback = True
+            r = cache[(p, q, I)]
+            if r["status"] != 0 or model_flags(r["coef"], p, q, I) != 3:
+                continue
+            aic = -2.0 * r["ll"] + float(2 * (p + q + I))
+            if aic < best_aic:
+                improving.append((aic, (p, q, I), r))
+        if trace is not None:
+            trace.append(list(nxt))
+        if not improving:
+            break
+        aic, (p, q, I), r = min(improving, key=lambda x: x[0])      # first minimum in list order
+        best_aic, best = aic, (p, q, I, r)
+        surround = []
+        for pd_ in (-1, 0, 1):
+            for qd in (-1, 0, 1):
+                inc = (1 - I) if (pd_ == 0 and qd == 0) else I
+                surround.append((p + pd_, q, inc))
+        nxt = [c for c in surround if c not in past and 0 <= c[0] <= max_p and 0 <= c[1] <= max_q]
+    if best is None:
+        out["status"] = ST_NO_MODEL
+        return out
+    p, q, I, r = best
+    out["order"] = (p, d, q, I)
+    out["coef"][:] = 0.0
+    out["coef"][: p + q + I] = r["coef"]
+    out["aic"] = best_aic
+    out["status"] = ST_CGD_FALLBACK if fallback else 0
+    return out
