@@ -21,6 +21,8 @@ collective; gloo carries only the timing barrier and the max-over-ranks reductio
                     over this rank's shard (strong scaling over --total-series, default 1M); unit series searched/sec
   --config c1       BASELINE.json configs[0]: ARIMA(1,0,1)+c on 10 000 series x 500 pts (the reference's CPU config)
   --config c4       BASELINE.json configs[3]: ARIMA(5,1,5)+c on 1M series x 4096 pts (the long-series path)
+  --config af       ARIMA.autoFit (ARIMA.scala:280-375) over C2-shaped series: KPSS choice of d, then the stepwise walk of
+                    css-cgd fits (arima_autofit_batch_device); unit series auto-fitted/sec, weak scaling
   --default-leg 0|1 c2, one GPU: also time the drop-in exactly as a caller gets it -- arima_fit_batch_device with the
                     ABI's default options, in a child process that keeps the box's GPU_MAX_HW_QUEUES (default 1)
   --device D        bind every rank to GPU D (also SPARKTS_DEVICE) instead of LOCAL_RANK's: several ranks on one GPU
@@ -55,6 +57,7 @@ sys.path.insert(0, os.path.join(ROOT, "spark-timeseries_amd"))
 CONFIGS = {
     # name: (p, d, q, intercept, T, base coefficients, jitter); c5 searches over C2-shaped series
     "c5": (2, 1, 2, 1, 1024, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05),
+    "af": (2, 1, 2, 1, 1024, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05),
     "c2": (2, 1, 2, 1, 1024, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05),
     "c1": (1, 0, 1, 1, 500, [3.5, 0.3, 0.7], 0.05),
     "c4": (5, 1, 5, 1, 4096, [0.1, 0.4, -0.2, 0.1, 0.05, -0.05, 0.3, 0.2, -0.1, 0.05, 0.05], 0.05),
@@ -375,7 +378,7 @@ def main():
 
     p, d, q, I, T, base, jitter = CONFIGS[args.config]
     if args.steps is None:                  # enough steps that the pipeline's fill is amortised (C2: 3 steps read
-        args.steps = {"c4": 5, "c5": 2}.get(args.config, 20)   # 9.35 M series/s, 20 steps 11.0, profiles/r04/zz_check)
+        args.steps = {"c4": 5, "c5": 2, "af": 3}.get(args.config, 20)   # 9.35 M series/s, 20 steps 11.0, profiles/r04/zz_check)
     if args.warmup is None:
         args.warmup = 1 if args.config == "c5" else 3
     if args.pipeline <= 0:
@@ -428,6 +431,8 @@ def main():
     eng.sample_device(series.data_ptr(), N, T, T, p, d, q, I, base, jitter, SEED, first)
     if args.config == "c5":
         return run_c5(args, eng, series, N, T, total_series, world, rank, dev, barrier, dist, max_over_ranks, scaling)
+    if args.config == "af":
+        return run_af(args, eng, series, N, T, total_series, world, rank, dev, barrier, dist, max_over_ranks, scaling)
     # one output set per fit context: pipelined steps never write the same buffers concurrently
     outs = [dict(coef=torch.empty((N, k), dtype=torch.float64, device=dev),
                  ll=torch.empty(N, dtype=torch.float64, device=dev),
@@ -715,6 +720,92 @@ def run_c5(args, eng, series, N, T, total_series, world, rank, dev, barrier, dis
             "roofline": roofline,
             "roofline_note": "per grid point (flops, evaluations, MaxEval fraction): tools/grid_profile.py",
             "parity": parity,
+            "cpu_baseline": cpu}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def run_af(args, eng, series, N, T, total_series, world, rank, dev, barrier, dist, max_over_ranks, scaling):
+    """ARIMA.autoFit per series (ARIMA.scala:280-375): a step = arima_autofit_batch_device over
+    this rank's shard, device-resident; parity = every rank's first rows against oracle.autofit, bit for bit."""
+    import numpy as np
+    import torch
+    from sparkts_amd.sharding import parity_over_ranks
+    out = dict(order=torch.empty((max(N, 1), 4), dtype=torch.int32, device=dev),
+               coef=torch.empty((max(N, 1), 11), dtype=torch.float64, device=dev),
+               aic=torch.empty(max(N, 1), dtype=torch.float64, device=dev),
+               status=torch.empty(max(N, 1), dtype=torch.int32, device=dev),
+               n_fits=torch.empty(max(N, 1), dtype=torch.int32, device=dev))
+
+    def step():
+        eng.autofit_device(series.data_ptr(), N, T, T, 5, 2, 5, out["order"].data_ptr(), out["coef"].data_ptr(),
+                           out["aic"].data_ptr(), out["status"].data_ptr(), out["n_fits"].data_ptr(), blocking=True)
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step()
+        log(f"[rank {rank}] autofit step {i} done at {time.perf_counter() - t0:.2f} s")
+    torch.cuda.synchronize(dev)
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t0, dist if world > 1 else None)
+    res = {k: v[:N].cpu().numpy() for k, v in out.items()}
+    fits = int(res["n_fits"].sum())
+    cpu, rows_checked, rows_ok = None, 0, 0
+    if args.cpu_seconds > 0 and N > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        affinity = len(os.sched_getaffinity(0))
+        host = series[: min(N, 256)].cpu().numpy()
+        t1 = time.perf_counter()
+        exp = []
+        for row in host:                                 # the restatement, one series at a time (bounded)
+            exp.append(O.autofit(row, 5, 2, 5))
+            if time.perf_counter() - t1 > args.cpu_seconds:
+                break
+        dt = time.perf_counter() - t1
+        rows_checked = len(exp)
+        for i, e in enumerate(exp):
+            coef_same = np.array_equal(res["coef"][i].view(np.int64), e["coef"].view(np.int64)) or \
+                (np.isnan(res["coef"][i]).all() and np.isnan(e["coef"]).all())
+            same = (res["status"][i] == e["status"] and tuple(res["order"][i]) == tuple(e["order"]) and
+                    res["n_fits"][i] == e["n_fits"] and coef_same and
+                    res["aic"][i].view(np.int64) == np.float64(e["aic"]).view(np.int64))
+            rows_ok += int(bool(same))
+        if world == 1:
+            phys = physical_cores()
+            cpu = {"value": rows_checked / dt, "unit": "series auto-fitted/sec", "cores": 1, "kind": "port",
+                   "host_physical_cores": phys, "projected_all_physical_cores": rows_checked / dt * phys if phys else None,
+                   "sample": f"the first {rows_checked} series of the shard through oracle.autofit (C restatement fits "
+                             f"and KPSS, the walk in Python) on one thread; not the spark-ts JVM"}
+    par = parity_over_ranks(rows_ok, rows_checked, dist if world > 1 else None)
+    if rank == 0:
+        st = res["status"]
+        sel = {}
+        for r in res["order"][: min(N, 65536)]:
+            key = f"({r[0]},{r[1]},{r[2]}){'+c' if r[3] == 1 else ''}" if r[0] >= 0 else "none"
+            sel[key] = sel.get(key, 0) + 1
+        print(json.dumps({
+            "metric": "series auto-fitted/sec, ARIMA.autoFit (KPSS d <= 2, stepwise p, q <= 5, css-cgd), x 1024 pts",
+            "value": total_series * args.steps / elapsed, "unit": "series auto-fitted/sec", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f64",
+            "data": f"synthetic C2-shaped series (ARIMAModel.sample semantics on device, seed {SEED})",
+            "config": {"workload": f"autoFit over {N} series x {T} pts per GPU (SURVEY.md 8(f) row 2)",
+                       "series_per_gpu": N, "series_total": total_series, "fits_per_series": fits / max(N, 1),
+                       "fits_per_sec": fits * world * args.steps / elapsed,
+                       "status_counts": {str(k): int(v) for k, v in zip(*np.unique(st, return_counts=True))},
+                       "selected_orders_top": dict(sorted(sel.items(), key=lambda kv: -kv[1])[:6]),
+                       "parallelism": f"series-sharded x{world}, no collective"},
+            "roofline": None,
+            "roofline_note": "autoFit's fits are k_cg_fit launches (roofline: the C2 line); the KPSS passes and the "
+                             "walk's gathers are HBM streams",
+            "parity": {"oracle_rows": par["oracle_rows"], "bit_identical": par["bit_identical"],
+                       "every_rank_bit_identical": par["every_rank_bit_identical"], "ranks_checked": par["ranks"],
+                       "checked": "status, (p, d, q, intercept), n_fits, coefficients and approxAIC, bit for bit"},
             "cpu_baseline": cpu}), flush=True)
     if world > 1:
         dist.barrier()

@@ -58,6 +58,12 @@ extern "C" {
 #define ARIMA_ST_ZERO_PARAMS         8  /* k == 0 parameters (ArithmeticException / index error)             */
 #define ARIMA_ST_UNSUPPORTED_METHOD  9  /* UnsupportedOperationException, ARIMA.scala:108 (and css-bobyqa)   */
 #define ARIMA_ST_SERIES_TOO_SHORT   10  /* negative lag-matrix size (NegativeArraySize / IndexOutOfBounds)    */
+/* ARIMA.autoFit outcomes (ARIMA.scala:280-375), arima_autofit_batch* only */
+#define ARIMA_ST_NOT_STATIONARY     11  /* no d <= max_d passes the KPSS test: "stationarity not achieved", :293-296 */
+#define ARIMA_ST_NO_MODEL           12  /* no candidate qualified: curBestModel stays null (NullPointerException)  */
+#define ARIMA_ST_CGD_FALLBACK       13  /* result returned, but a css-cgd candidate failed in the optimizer where the
+                                           reference retries with css-bobyqa (:315-319; not built): the selection
+                                           treats that retry as failed too, so it may differ from the reference's  */
 
 /* ---- fit methods (ARIMA.scala:105-109) -------------------------------------------------------------- */
 #define ARIMA_METHOD_CSS_CGD     0
@@ -199,6 +205,27 @@ int arima_order_search_batch_device(arima_handle *h, const double *d_series, int
                                     int64_t ld, int32_t max_p, int32_t max_d, int32_t max_q,
                                     int32_t intercept_mode, int32_t method, int32_t *d_order_out,
                                     double *d_coef_out, double *d_aic_out, void *stream);
+
+/* ---- ARIMA.autoFit over a batch (ARIMA.scala:280-375; python/sparkts/models/ARIMA.py:25-60 `autofit`) --------- *
+ * Per series: d = the first of 0..max_d whose differencesOfOrderD(ts, d) (NOT dropped) passes kpsstest(_, "c") at 5 %
+ * (TimeSeriesStatisticalTests.scala:369-395); then findBestARMAModel's stepwise walk over (p, q, intercept) on that
+ * differenced series with css-cgd fits (intercept only for d <= 1; the neighbourhood never changes q -- the
+ * reference's quirks, ARIMA.scala:298-300, :356-366), keeping the first minimum approxAIC among stationary and
+ * invertible fits. max_p, max_q <= 5. order_out N x 4 = (p, d, q, intercept) (-1s when the series has no model),
+ * coef_out N x 11 (zero-padded; NaN when none), aic_out N (+inf when none), status_out N: ARIMA_ST_OK,
+ * ARIMA_ST_CGD_FALLBACK (result valid, see above), ARIMA_ST_NOT_STATIONARY, ARIMA_ST_NO_MODEL, or the KPSS
+ * regression's shape status (T <= 1). n_fits_out (nullable): candidate fits the walk ran for the series.        */
+int arima_autofit_batch(arima_handle *h, const double *series, int64_t n_series, int32_t T, int32_t max_p,
+                        int32_t max_d, int32_t max_q, int32_t *order_out, double *coef_out, double *aic_out,
+                        int32_t *status_out, int32_t *n_fits_out);
+int arima_autofit_batch_device(arima_handle *h, const double *d_series, int64_t n_series, int32_t T, int64_t ld,
+                               int32_t max_p, int32_t max_d, int32_t max_q, int32_t *d_order_out,
+                               double *d_coef_out, double *d_aic_out, int32_t *d_status_out, int32_t *d_n_fits_out,
+                               void *stream);
+/* TimeSeriesStatisticalTests.kpsstest(ts, "c") (TimeSeriesStatisticalTests.scala:369-393) per series: stat_out N,
+ * status_out N (ARIMA_ST_OK, or the OLS shape status for T <= 1). Host buffers.                                  */
+int arima_kpss_batch(arima_handle *h, const double *series, int64_t n_series, int32_t T, double *stat_out,
+                     int32_t *status_out);
 
 /* ---- synthetic workload generator (ARIMAModel.sample semantics, ARIMA.scala:655-678) ---------------- *
  * Writes N x T series (row stride ld) into device memory: per-series coefficients = base +/- U(0, jitter)

@@ -238,7 +238,18 @@ def find_roots(coefficients):
 
 
 def _all_roots_outside_unit_circle(poly):
-    roots = find_roots(poly)
+    """`!findRoots(poly).exists(_.abs() <= 1.0)` (ARIMA.scala:812-815). Degenerate polynomials, where the reference's
+    companion matrix holds infinities or NaNs and commons EigenDecomposition's outcome is not pinned by any test,
+    follow the device's rule (arima_device.hpp roots_outside_unit_circle): a non-finite coefficient -> False; a zero
+    leading coefficient is a root at infinity (outside), so the degree drops (for p = 1 this is exactly the
+    reference: the 1 x 1 companion [-Inf] has |root| = Inf)."""
+    poly = np.asarray(poly, dtype=np.float64)
+    if not np.all(np.isfinite(poly)):
+        return False
+    n = len(poly) - 1
+    while n >= 1 and poly[n] == 0.0:
+        n -= 1
+    roots = find_roots(poly[: n + 1])
     return not np.any(np.abs(roots) <= 1.0)
 
 

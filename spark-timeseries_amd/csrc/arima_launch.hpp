@@ -58,6 +58,36 @@ constexpr int kFitBlocksPerCU = kFitWavesPerCU / kFitBlockWaves;
 
 constexpr int kMergeLiveDefault = 16;        // k_cg_fit's drain merge threshold (option "merge_live"; 0 = off)
 
+// ---- ARIMA.autoFit (arima_autofit.hip) ----
+constexpr int kAfCombos = 36;      // candidate (p, q, intercept) orders the stepwise walk can meet: p <= 5, q <= 2
+constexpr int kAfMaxCand = 4;      // distinct candidates of one round of one series
+struct AfSeries {                  // one series' walk state (findBestARMAModel's locals, ARIMA.scala:321-375)
+    double best_aic;               // curBestAIC
+    unsigned long long seen;       // pastParams, one bit per (p, q, intercept)
+    int32_t dsel;                  // d chosen by the KPSS search (-1: none)
+    int32_t status;                // ARIMA_ST_*
+    int32_t best;                  // packed p | q << 4 | I << 8 of curBestModel, -1 = null
+    int32_t n_fits;                // candidate fits run so far
+    int32_t fallback;              // a css-cgd candidate threw where the reference tries css-bobyqa
+    int32_t ncand;                 // candidates of the current round (0: the walk is over)
+    int32_t cand[kAfMaxCand];      // nextParams, packed, deduplicated in first-appearance order
+    int32_t slot[kAfMaxCand];      // each candidate's row in its order's list this round
+};
+int launch_kpss_c(const double *w, int64_t ld, int n, int64_t N, int d, int32_t *dsel, double *stat_out, hipStream_t s);
+int kpss_lag_host(int n);
+int kpss_lag_max();
+int launch_difference_sel(const double *in, int64_t ld_in, double *out, int64_t ld_out, int64_t N, int T,
+                          const int32_t *dsel, int d, hipStream_t s);
+int launch_af_init(int64_t N, const int32_t *dsel, AfSeries *st, int32_t kpss_status, hipStream_t s);
+int launch_af_plan(int64_t N, AfSeries *st, unsigned *counts, int32_t *lists, hipStream_t s);
+int launch_gather_rows(const double *in, int64_t ld, const int32_t *list, int64_t count, int T, double *out,
+                       hipStream_t s);
+int launch_af_update(int64_t N, AfSeries *st, const int64_t *off, const double *res_coef, const double *res_ll,
+                     const int32_t *res_status, const uint8_t *res_flags, double *best_coef, int max_p, int max_q,
+                     hipStream_t s);
+int launch_af_finish(int64_t N, const AfSeries *st, const double *best_coef, int32_t *order_out, double *coef_out,
+                     double *aic_out, int32_t *status_out, int32_t *n_fits_out, hipStream_t s);
+
 int hr_shape_status_host(int n, int p, int q, int I);
 int ar_shape_status_host(int n, int p, int I);
 

@@ -170,6 +170,11 @@ struct arima_handle {
     SearchLane lanes[kMaxSearchLanes];
     DevBuf os_order;
     unsigned long long *search_acc_host = nullptr;   // pinned: (kCtlWords + 1) words per lane of the last search
+    // autoFit (arima_autofit_batch*): the differenced rows, the walk state, the rounds' per-order lists and results
+    DevBuf af_rows, af_dsel, af_state, af_best, af_counts, af_lists, af_off, af_coef, af_ll, af_status, af_flags;
+    DevBuf af_out_order, af_out_coef, af_out_aic, af_out_status, af_out_nfits;   // host-API staging
+    int64_t *af_host = nullptr;                      // pinned: kAfCombos counts, then kAfCombos row offsets
+    hipEvent_t ev_af = nullptr;
     int search_lanes_used = 0;
     int64_t search_n = 0, search_fits = 0;
 };
@@ -360,6 +365,8 @@ int arima_destroy(arima_handle *h) {
             if (e) hipEventDestroy(e);
     if (h->slot_ctl) hipHostFree(h->slot_ctl);
     if (h->search_acc_host) hipHostFree(h->search_acc_host);
+    if (h->af_host) hipHostFree(h->af_host);
+    if (h->ev_af) hipEventDestroy(h->ev_af);
     for (auto &e : h->ev)
         if (e) hipEventDestroy(e);
     if (h->ev_done) hipEventDestroy(h->ev_done);
@@ -1497,6 +1504,203 @@ int arima_order_search_batch(arima_handle *h, const double *series, int64_t N, i
     HIPCHK(h, hipStreamSynchronize(s));
     if (rc != ARIMA_OK) return rc;
     return take_fault(h);
+}
+
+// ---------------------------------------------------------------------------------------------------------
+// ARIMA.autoFit over a batch (ARIMA.scala:280-375; arima_autofit.hip has the kernels and the quirks they restate)
+// ---------------------------------------------------------------------------------------------------------
+// Host loop: (1) the KPSS search over d = 0..max_d (rows of undecided series differenced at d into af_rows, then the
+// test; decided rows keep their d); (2) rounds of the stepwise walk: k_af_plan appends every walking series'
+// candidates to per-(p, q, intercept) lists, the host reads the list sizes (one small copy per round), and every
+// non-empty list is gathered and fitted as one batch (fit_kernels: AR-only OLS or HR init + k_cg_fit) on the fit
+// contexts' streams, several orders at once; k_af_update then picks each series' new incumbent and neighbourhood.
+// The walk ends when no series has candidates left (at most max_p + 2 rounds after the first).
+constexpr int kAfContexts = 4;                     // fit contexts the orders of one round rotate over
+
+static int autofit_locked(arima_handle *h, const double *d_series, int64_t N, int32_t T, int64_t ld, int32_t max_p,
+                          int32_t max_d, int32_t max_q, int32_t *d_order, double *d_coef, double *d_aic,
+                          int32_t *d_status, int32_t *d_nfits, hipStream_t s, int64_t *fits_out) {
+    using sts::kAfCombos;
+    if (max_p < 0 || max_q < 0 || max_d < 0) return set_err(h, ARIMA_E_INVALID_ARG, "bad autofit bounds");
+    if (max_p > 5 || max_q > 5 || max_d > kMaxD) return set_err(h, ARIMA_E_UNSUPPORTED, "p, q <= 5, d <= 16");
+    if (N < 0 || T < 0 || ld < T || (N > 0 && (!d_series || !d_order || !d_coef || !d_aic || !d_status)))
+        return set_err(h, ARIMA_E_INVALID_ARG, "bad shape");
+    h->stats = arima_fit_stats{};
+    h->stats_ctx = -1;
+    if (N == 0) return ARIMA_OK;
+    if (sts::kpss_lag_host(T) > sts::kpss_lag_max())
+        return set_err(h, ARIMA_E_UNSUPPORTED, "KPSS lag > 32 (series longer than ~19 900 points)");
+    HIPCHK(h, hipSetDevice(h->device));
+    const int64_t ldT = row_stride(h, T);
+    const int64_t rows_max = N * sts::kAfMaxCand;  // candidate fits of one round, at most
+    RCCHK(h, h->af_rows.ensure((size_t)N * ldT * sizeof(double)), "autofit workspace");
+    RCCHK(h, h->af_dsel.ensure((size_t)N * sizeof(int32_t)), "autofit workspace");
+    RCCHK(h, h->af_state.ensure((size_t)N * sizeof(sts::AfSeries)), "autofit workspace");
+    RCCHK(h, h->af_best.ensure((size_t)N * 11 * sizeof(double)), "autofit workspace");
+    RCCHK(h, h->af_counts.ensure(kAfCombos * sizeof(unsigned)), "autofit workspace");
+    RCCHK(h, h->af_off.ensure(kAfCombos * sizeof(int64_t)), "autofit workspace");
+    RCCHK(h, h->af_lists.ensure((size_t)kAfCombos * N * sizeof(int32_t)), "autofit workspace");
+    RCCHK(h, h->af_coef.ensure((size_t)rows_max * 11 * sizeof(double)), "autofit workspace");
+    RCCHK(h, h->af_ll.ensure((size_t)rows_max * sizeof(double)), "autofit workspace");
+    RCCHK(h, h->af_status.ensure((size_t)rows_max * sizeof(int32_t)), "autofit workspace");
+    RCCHK(h, h->af_flags.ensure((size_t)rows_max), "autofit workspace");
+    if (!h->af_host && hipHostMalloc((void **)&h->af_host, 2 * kAfCombos * sizeof(int64_t), 0) != hipSuccess)
+        return set_err(h, ARIMA_E_OOM, "pinned");
+    if (!h->ev_af) HIPCHK(h, hipEventCreateWithFlags(&h->ev_af, hipEventDisableTiming));
+    const int P = std::min(kAfContexts, kMaxPipeline);
+    for (int j = 0; j < P; ++j) {                  // every context's gather buffer and fit workspace at full size
+        FitCtx &c = h->fctx[j];
+        RCCHK(h, c.diff.ensure((size_t)N * ldT * sizeof(double)), "autofit workspace");
+        RCCHK(h, c.ws.init.ensure((size_t)N * 11 * sizeof(double)), "workspace");
+        RCCHK(h, c.ws.hr_status.ensure((size_t)N * sizeof(int32_t)), "workspace");
+        RCCHK(h, c.ws.ctl.ensure(kCtlWords * sizeof(unsigned long long)), "workspace");
+        RCCHK(h, c.ws.xring.ensure(sts::kExpressRingBytes), "workspace");
+        RCCHK(h, c.ws.xready.ensure(sts::kExpressReadyBytes), "workspace");
+        if (c.has_done) HIPCHK(h, hipStreamWaitEvent(s, c.ev_done, 0));
+    }
+    HIPCHK(h, hipEventRecord(h->ev[0], s));
+    // (1) d: the first of 0..max_d whose differencesOfOrderD(ts, d) passes kpsstest(_, "c") (ARIMA.scala:287-297)
+    const int32_t kpss_st = T <= 0 ? ARIMA_ST_NO_DATA : (T < 2 ? ARIMA_ST_NOT_ENOUGH_DATA : ARIMA_ST_OK);
+    int32_t *dsel = h->af_dsel.as<int32_t>();
+    HIPCHK(h, hipMemsetAsync(dsel, 0xff, (size_t)N * sizeof(int32_t), s));
+    if (kpss_st == ARIMA_ST_OK) {
+        for (int d = 0; d <= max_d; ++d) {
+            RCCHK(h, sts::launch_difference_sel(d_series, ld, h->af_rows.as<double>(), ldT, N, T, dsel, d, s),
+                  "difference");
+            RCCHK(h, sts::launch_kpss_c(h->af_rows.as<double>(), ldT, T, N, d, dsel, nullptr, s), "kpss");
+        }
+    }
+    // (2) the stepwise walk (findBestARMAModel, :310-375) on each series' differenced row
+    sts::AfSeries *st = h->af_state.as<sts::AfSeries>();
+    RCCHK(h, sts::launch_af_init(N, dsel, st, kpss_st, s), "autofit init");
+    int64_t fits = 0;
+    for (int round = 0; kpss_st == ARIMA_ST_OK; ++round) {
+        HIPCHK(h, hipMemsetAsync(h->af_counts.ptr, 0, kAfCombos * sizeof(unsigned), s));
+        RCCHK(h, sts::launch_af_plan(N, st, h->af_counts.as<unsigned>(), h->af_lists.as<int32_t>(), s), "autofit plan");
+        unsigned counts[kAfCombos];
+        HIPCHK(h, hipMemcpyAsync(h->af_host, h->af_counts.ptr, kAfCombos * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipStreamSynchronize(s));
+        memcpy(counts, h->af_host, sizeof counts);
+        int64_t *off = h->af_host + kAfCombos;
+        int64_t total = 0;
+        for (int cb = 0; cb < kAfCombos; ++cb) {
+            off[cb] = total;
+            total += counts[cb];
+        }
+        if (total == 0) break;
+        fits += total;
+        HIPCHK(h, hipMemcpyAsync(h->af_off.ptr, off, kAfCombos * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        HIPCHK(h, hipEventRecord(h->ev_af, s));
+        // the round's orders, largest list first, over the fit contexts (several orders fit at once)
+        int order[kAfCombos];
+        for (int cb = 0; cb < kAfCombos; ++cb) order[cb] = cb;
+        std::stable_sort(order, order + kAfCombos, [&](int a, int b) { return counts[a] > counts[b]; });
+        int used = 0;
+        for (int oi = 0; oi < kAfCombos && counts[order[oi]] > 0; ++oi) {
+            const int cb = order[oi];
+            const int p = (cb / 2) / 3, q = (cb / 2) % 3, I = cb % 2;
+            const int64_t cnt = counts[cb];
+            FitCtx &c = h->fctx[used % P];
+            HIPCHK(h, hipStreamWaitEvent(c.stream, h->ev_af, 0));
+            RCCHK(h, sts::launch_gather_rows(h->af_rows.as<double>(), ldT, h->af_lists.as<int32_t>() + (int64_t)cb * N,
+                                             cnt, T, c.diff.as<double>(), c.stream), "gather");
+            int64_t gridb = 0, xb = 0;
+            // fitModel(p, 0, q, diffedTs, intercept, "css-cgd") (:316); rows of order cb from off[cb] (coef stride k)
+            RCCHK(h, fit_kernels(h, c.ws, c.diff.as<double>(), ldT, T, cnt, p, q, I, ARIMA_METHOD_CSS_CGD, nullptr,
+                                 h->af_coef.as<double>() + off[cb] * 11, h->af_ll.as<double>() + off[cb],
+                                 h->af_status.as<int32_t>() + off[cb], nullptr, nullptr,
+                                 h->af_flags.as<uint8_t>() + off[cb], c.stream, nullptr, &gridb, &xb, P > 1), "fit");
+            HIPCHK(h, end_fit(c, c.stream));
+            ++used;
+        }
+        for (int j = 0; j < std::min(used, P); ++j) HIPCHK(h, hipStreamWaitEvent(s, h->fctx[j].ev_done, 0));
+        RCCHK(h, sts::launch_af_update(N, st, h->af_off.as<int64_t>(), h->af_coef.as<double>(), h->af_ll.as<double>(),
+                                       h->af_status.as<int32_t>(), h->af_flags.as<uint8_t>(), h->af_best.as<double>(),
+                                       max_p, max_q, s), "autofit update");
+        if (round > 64) return set_err(h, ARIMA_E_DEVICE, "autofit: the walk did not end");
+    }
+    RCCHK(h, sts::launch_af_finish(N, st, h->af_best.as<double>(), d_order, d_coef, d_aic, d_status, d_nfits, s),
+          "autofit finish");
+    HIPCHK(h, hipEventRecord(h->ev[3], s));
+    h->stats.n_series = fits;
+    if (fits_out) *fits_out = fits;
+    return ARIMA_OK;
+}
+
+int arima_autofit_batch_device(arima_handle *h, const double *d_series, int64_t n_series, int32_t T, int64_t ld,
+                               int32_t max_p, int32_t max_d, int32_t max_q, int32_t *d_order_out,
+                               double *d_coef_out, double *d_aic_out, int32_t *d_status_out, int32_t *d_n_fits_out,
+                               void *stream) {
+    if (!h) return ARIMA_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    hipStream_t s = stream ? (hipStream_t)stream : h->stream;
+    begin_call(h, s);
+    const int rc = autofit_locked(h, d_series, n_series, T, ld, max_p, max_d, max_q, d_order_out, d_coef_out,
+                                  d_aic_out, d_status_out, d_n_fits_out, s, nullptr);
+    HIPCHK(h, end_call(h, s));
+    return rc;
+}
+
+int arima_autofit_batch(arima_handle *h, const double *series, int64_t N, int32_t T, int32_t max_p, int32_t max_d,
+                        int32_t max_q, int32_t *order_out, double *coef_out, double *aic_out, int32_t *status_out,
+                        int32_t *n_fits_out) {
+    if (!h) return ARIMA_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (N < 0 || T < 0) return set_err(h, ARIMA_E_INVALID_ARG, "bad shape");
+    if (N == 0) return ARIMA_OK;
+    if (!series || !order_out || !coef_out || !aic_out || !status_out) return set_err(h, ARIMA_E_INVALID_ARG, "null buffer");
+    HIPCHK(h, hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    begin_call(h, s);
+    RCCHK(h, h->h_series.ensure((size_t)N * std::max(T, 1) * sizeof(double)), "staging");
+    RCCHK(h, h->af_out_order.ensure((size_t)N * 4 * sizeof(int32_t)), "staging");
+    RCCHK(h, h->af_out_coef.ensure((size_t)N * 11 * sizeof(double)), "staging");
+    RCCHK(h, h->af_out_aic.ensure((size_t)N * sizeof(double)), "staging");
+    RCCHK(h, h->af_out_status.ensure((size_t)N * sizeof(int32_t)), "staging");
+    RCCHK(h, h->af_out_nfits.ensure((size_t)N * sizeof(int32_t)), "staging");
+    if (T > 0) HIPCHK(h, hipMemcpyAsync(h->h_series.ptr, series, (size_t)N * T * sizeof(double), hipMemcpyHostToDevice, s));
+    int rc = autofit_locked(h, h->h_series.as<double>(), N, T, T, max_p, max_d, max_q, h->af_out_order.as<int32_t>(),
+                            h->af_out_coef.as<double>(), h->af_out_aic.as<double>(), h->af_out_status.as<int32_t>(),
+                            h->af_out_nfits.as<int32_t>(), s, nullptr);
+    if (rc == ARIMA_OK) {
+        HIPCHK(h, hipMemcpyAsync(order_out, h->af_out_order.ptr, (size_t)N * 4 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipMemcpyAsync(coef_out, h->af_out_coef.ptr, (size_t)N * 11 * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipMemcpyAsync(aic_out, h->af_out_aic.ptr, (size_t)N * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipMemcpyAsync(status_out, h->af_out_status.ptr, (size_t)N * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        if (n_fits_out)
+            HIPCHK(h, hipMemcpyAsync(n_fits_out, h->af_out_nfits.ptr, (size_t)N * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(h, end_call(h, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    if (rc != ARIMA_OK) return rc;
+    return take_fault(h);
+}
+
+int arima_kpss_batch(arima_handle *h, const double *series, int64_t N, int32_t T, double *stat_out, int32_t *status_out) {
+    if (!h || N < 0 || T < 0) return ARIMA_E_INVALID_ARG;
+    std::lock_guard<std::mutex> lk(h->mu);
+    if (N == 0) return ARIMA_OK;
+    if (!series || !stat_out || !status_out) return set_err(h, ARIMA_E_INVALID_ARG, "null buffer");
+    const int32_t st = T <= 0 ? ARIMA_ST_NO_DATA : (T < 2 ? ARIMA_ST_NOT_ENOUGH_DATA : ARIMA_ST_OK);
+    if (st == ARIMA_ST_OK && sts::kpss_lag_host(T) > sts::kpss_lag_max())
+        return set_err(h, ARIMA_E_UNSUPPORTED, "KPSS lag > 32 (series longer than ~19 900 points)");
+    HIPCHK(h, hipSetDevice(h->device));
+    hipStream_t s = h->stream;
+    begin_call(h, s);
+    RCCHK(h, h->h_ll.ensure((size_t)N * sizeof(double)), "staging");
+    if (st == ARIMA_ST_OK) {
+        int64_t ld = 0;
+        RCCHK(h, upload_padded(h, series, N, T, &ld, s), "upload");
+        RCCHK(h, sts::launch_kpss_c(h->diff.as<double>(), ld, T, N, 0, nullptr, h->h_ll.as<double>(), s), "kpss");
+        HIPCHK(h, hipMemcpyAsync(stat_out, h->h_ll.ptr, (size_t)N * sizeof(double), hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(h, end_call(h, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    for (int64_t i = 0; i < N; ++i) {
+        status_out[i] = st;
+        if (st != ARIMA_ST_OK) stat_out[i] = NAN;
+    }
+    return ARIMA_OK;
 }
 
 int arima_sample_batch_device(arima_handle *h, double *d_series, int64_t N, int32_t T, int64_t ld, int32_t p,

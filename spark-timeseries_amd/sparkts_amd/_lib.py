@@ -29,6 +29,9 @@ ST_BAD_INTERVAL = 7
 ST_ZERO_PARAMS = 8
 ST_UNSUPPORTED_METHOD = 9
 ST_SERIES_TOO_SHORT = 10
+ST_NOT_STATIONARY = 11      # autoFit: no d <= max_d passes KPSS
+ST_NO_MODEL = 12            # autoFit: no candidate qualified
+ST_CGD_FALLBACK = 13        # autoFit: a css-cgd candidate failed where the reference retries with css-bobyqa
 
 METHOD_CSS_CGD = 0
 METHOD_CSS_BOBYQA = 1
@@ -48,7 +51,8 @@ EXPORTED = [
     "arima_difference_batch", "arima_inverse_difference_batch", "arima_css_loglik_batch",
     "arima_css_gradient_batch", "arima_hannan_rissanen_batch", "arima_forecast_batch", "arima_model_flags_batch",
     "arima_sample_batch_device", "arima_order_search_batch", "arima_order_search_batch_device",
-    "arima_forecast_batch_device", "arima_synchronize",
+    "arima_forecast_batch_device", "arima_synchronize", "arima_autofit_batch", "arima_autofit_batch_device",
+    "arima_kpss_batch",
 ]
 
 
@@ -141,6 +145,10 @@ def load():
         L.arima_order_search_batch.argtypes = [H, _dp, _i64, _i32, _i32, _i32, _i32, _i32, _i32, _i32p, _dp, _dp]
         L.arima_order_search_batch_device.argtypes = [H, _vp, _i64, _i32, _i64, _i32, _i32, _i32, _i32, _i32, _vp,
                                                       _vp, _vp, _vp]
+        L.arima_autofit_batch.argtypes = [H, _dp, _i64, _i32, _i32, _i32, _i32, _i32p, _dp, _dp, _i32p, _i32p]
+        L.arima_autofit_batch_device.argtypes = [H, _vp, _i64, _i32, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp,
+                                                 _vp]
+        L.arima_kpss_batch.argtypes = [H, _dp, _i64, _i32, _dp, _i32p]
         _lib = L
         return L
 
@@ -334,6 +342,38 @@ class Engine:
                                                     method, _ptr(order, _i32p), _ptr(coef), _ptr(aic)),
                     "arima_order_search_batch")
         return order, coef, aic
+
+    def autofit(self, series, max_p=5, max_d=2, max_q=5):
+        """ARIMA.autoFit per series (see include/sparkts_arima.h). Returns dict(order N x 4 (p, d, q, intercept),
+        coef N x 11, aic N, status N, n_fits N)."""
+        series = np.ascontiguousarray(np.atleast_2d(series), dtype=np.float64)
+        N, T = series.shape
+        out = dict(order=np.empty((N, 4), dtype=np.int32), coef=np.empty((N, 11)), aic=np.empty(N),
+                   status=np.empty(N, dtype=np.int32), n_fits=np.empty(N, dtype=np.int32))
+        self._check(self.L.arima_autofit_batch(self.h, _ptr(series), N, T, max_p, max_d, max_q,
+                                               _ptr(out["order"], _i32p), _ptr(out["coef"]), _ptr(out["aic"]),
+                                               _ptr(out["status"], _i32p), _ptr(out["n_fits"], _i32p)),
+                    "arima_autofit_batch")
+        return out
+
+    def autofit_device(self, d_series, n_series, T, ld, max_p, max_d, max_q, d_order, d_coef, d_aic, d_status,
+                       d_n_fits=None, stream=None, blocking=True):
+        """Device-pointer autoFit (ints = raw HBM addresses)."""
+        self._check(self.L.arima_autofit_batch_device(self.h, d_series, n_series, T, ld, max_p, max_d, max_q, d_order,
+                                                      d_coef, d_aic, d_status, d_n_fits, stream),
+                    "arima_autofit_batch_device")
+        if blocking:
+            self.synchronize()
+
+    def kpss(self, series):
+        """TimeSeriesStatisticalTests.kpsstest(ts, "c") per series: (stat N, status N)."""
+        series = np.ascontiguousarray(np.atleast_2d(series), dtype=np.float64)
+        N, T = series.shape
+        stat = np.empty(N)
+        st = np.empty(N, dtype=np.int32)
+        self._check(self.L.arima_kpss_batch(self.h, _ptr(series), N, T, _ptr(stat), _ptr(st, _i32p)),
+                    "arima_kpss_batch")
+        return stat, st
 
     def model_flags(self, coef, p, q, include_intercept):
         k = p + q + (1 if include_intercept else 0)

@@ -53,6 +53,19 @@ class IndexOutOfBoundsException(ARIMAFitError):
     pass
 
 
+class StationarityNotAchieved(ARIMAFitError):
+    """autoFit: `throw new Exception(s"stationarity not achieved with differencing order <= $maxD")` (ARIMA.scala:295)."""
+
+
+class NullPointerException(ARIMAFitError):
+    """autoFit: no candidate model qualified, so `bestModel.p` dereferences null (ARIMA.scala:302-304)."""
+
+
+class BobyqaFallbackUnavailable(ARIMAFitError):
+    """autoFit: a css-cgd candidate failed where the reference retries it with css-bobyqa (ARIMA.scala:315-319),
+    which this build does not have; the selection it returned assumes that retry failed too."""
+
+
 _EXC = {
     _lib.ST_MAX_EVAL: TooManyEvaluationsException,
     _lib.ST_BRACKET_MAX_EVAL: TooManyEvaluationsException,
@@ -64,6 +77,9 @@ _EXC = {
     _lib.ST_ZERO_PARAMS: ArithmeticException,
     _lib.ST_UNSUPPORTED_METHOD: UnsupportedOperationException,
     _lib.ST_SERIES_TOO_SHORT: IndexOutOfBoundsException,
+    _lib.ST_NOT_STATIONARY: StationarityNotAchieved,
+    _lib.ST_NO_MODEL: NullPointerException,
+    _lib.ST_CGD_FALLBACK: BobyqaFallbackUnavailable,
 }
 
 
@@ -81,9 +97,44 @@ def _method_code(method):
     return _lib.METHODS[method]
 
 
-# ARIMA.autoFit (ARIMA.scala:280-375; python/sparkts/models/ARIMA.py autofit) is deliberately not mirrored: it picks d
-# with the KPSS stationarity test (TimeSeriesStatisticalTests, outside SURVEY.md 8's scope) and then runs a
-# stepwise (p, q, intercept) search. The batched exhaustive grid that covers config C5 is order_search() below.
+def autofit(ts, maxp=5, maxd=2, maxq=5, sc=None, device=None, strict=False):
+    """ARIMA.autoFit (ARIMA.scala:280-375), the reference binding's `autofit` (python/sparkts/models/ARIMA.py:25-60):
+    d from the KPSS test, then the stepwise (p, q, intercept) walk with css-cgd fits. Raises what the reference
+    throws (StationarityNotAchieved, NullPointerException, the KPSS regression's MathIllegalArgumentException). A
+    result whose walk met a css-cgd failure the reference would retry with css-bobyqa is returned (the retry counted as
+    failed) unless strict=True, which raises BobyqaFallbackUnavailable instead."""
+    ts = np.asarray(ts, dtype=np.float64).ravel()
+    r = autofit_models(ts[None, :], maxp, maxd, maxq, device=device)
+    st = int(r.status[0])
+    if st != _lib.ST_OK and not (st == _lib.ST_CGD_FALLBACK and not strict):
+        raise_for_status(st)
+    return r.model(0, strict=strict)
+
+
+class AutoFitBatchResult:
+    """Per-series outputs of a batched autoFit (the arrays arima_autofit_batch fills)."""
+
+    def __init__(self, r, device):
+        self.order = r["order"]
+        self.coefficients = r["coef"]
+        self.aic = r["aic"]
+        self.status = r["status"]
+        self.n_fits = r["n_fits"]
+        self._device = device
+
+    def model(self, i, strict=False):
+        st = int(self.status[i])
+        if st != _lib.ST_OK and not (st == _lib.ST_CGD_FALLBACK and not strict):
+            raise_for_status(st)
+        p, d, q, I = (int(v) for v in self.order[i])
+        return ARIMAModel(p, d, q, self.coefficients[i, :p + q + I], bool(I), device=self._device)
+
+
+def autofit_models(series, maxp=5, maxd=2, maxq=5, device=None):
+    """Batched ARIMA.autoFit over (N, T) series (one call per partition bucket, the mapSeries drop-in for autofit).
+    Never raises for per-series outcomes; inspect `.status`."""
+    eng = _lib.Engine.get(device)
+    return AutoFitBatchResult(eng.autofit(series, maxp, maxd, maxq), device)
 
 
 def fit_model(p, d, q, ts, includeIntercept=True, method="css-cgd", userInitParams=None, sc=None, device=None):

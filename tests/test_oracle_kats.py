@@ -161,3 +161,66 @@ def test_status_semantics():
     assert O.fit(np.arange(30.0), 0, 0, 0, intercept=False)["status"] == 6
     # unknown method after a successful HR init -> UnsupportedOperationException
     assert O.fit(DS1, 1, 0, 1, method=1)["status"] == 9
+
+
+KPSS_R_V = [0.0187461709418264, -0.184252542069064, -1.37133054992251, -0.599167715783718,
+            0.294545126567508, 0.389794300700167, -1.20807617542949, -0.363676017470862,
+            -1.62667268170309, -0.256478394123992, 1.10177950308713, 0.755781508027337,
+            -0.238233556018718, 0.98744470341339, 0.741390128383824, 0.0893472664958216,
+            -0.954943856152377, -0.195150384667239, 0.92552126209408, 0.482978524836611]
+
+
+def test_kpss_r_equivalence():
+    # TimeSeriesStatisticalTestsSuite.scala:102-142 (R tseries::kpss.test on set.seed(10); rnorm(20)): Level 0.27596,
+    # Trend 0.05092, within 1e-4
+    st, c = O.kpss(KPSS_R_V, "c")
+    st2, ct = O.kpss(KPSS_R_V, "ct")
+    assert st == 0 and st2 == 0
+    assert abs(c - 0.2759) < 1e-4 and abs(ct - 0.05092) < 1e-4
+    # the OLS shape check: one regressor needs at least two rows (AbstractMultipleLinearRegression.validateSampleData)
+    assert O.kpss([1.0], "c")[0] == 5 and O.kpss([], "c")[0] == 6
+
+
+def _autofit_kat_series():
+    # ARIMASuite.scala:181-185: ARIMAModel(2, 0, 0, [2.5, 0.4, 0.3], true).sample(250, new MersenneTwister(10L))
+    sampled = O.add_time_dependent_effects(mt_gauss(10, 250), 2, 0, 0, 1, [2.5, 0.4, 0.3])
+    return sampled, O.inverse_differences_of_order_d(sampled, 5)
+
+
+def test_autofit_kats():
+    # ARIMASuite.scala:181-211
+    sampled, high_i = _autofit_kat_series()
+    assert O.autofit(high_i)["status"] == O.ST_NOT_STATIONARY          # Try(autoFit(highI)).isFailure
+    r10 = O.autofit(high_i, max_d=10)                                   # Try(autoFit(highI, maxD = 10)).isSuccess
+    assert r10["status"] == 0 and r10["order"][1] >= 1
+    r = O.autofit(sampled, 5, 2, 5)
+    assert r["status"] == 0
+    p, d, q, I = r["order"]
+    k = p + q + I
+    fitted_aic = -2 * O.loglik_css(sampled, p, d, q, I, r["coef"][:k]) + 2 * k      # fitted.approxAIC(sampled)
+    ji = O.fit(sampled, 0, d, 0, True)                                  # fitModel(0, fitted.d, 0, sampled)
+    ji_aic = -2 * O.loglik_css(sampled, 0, d, 0, 1, ji["coef"]) + 2
+    assert ji_aic > fitted_aic
+
+
+def test_autofit_walk_quirks():
+    # findBestARMAModel restated with its quirks (ARIMA.scala:310-375): the first round fits (0,0), (2,2), (1,0), (0,1)
+    # with the d-dependent intercept; later rounds vary p and flip the intercept, never q; a candidate is fitted once
+    sampled, _ = _autofit_kat_series()
+    trace = []
+    r = O.autofit(sampled, 5, 2, 5, trace=trace)
+    assert trace[0] == [(0, 0, 1), (2, 2, 1), (1, 0, 1), (0, 1, 1)]
+    q_first = {c[1] for c in trace[0]}
+    for rnd in trace[1:]:
+        assert len({c[1] for c in rnd}) == 1 and rnd[0][1] in q_first      # one q per later round
+    assert r["n_fits"] == len({c for rnd in trace for c in rnd})
+    # d = 2 (two unit roots): no intercept in the walk (addIntercept = d <= 1, :300)
+    rw2 = O.inverse_differences_of_order_d(sampled, 2)
+    tr2 = []
+    r2 = O.autofit(rw2, 5, 2, 5, trace=tr2)
+    assert r2["order"][1] == 2 and tr2[0][0] == (0, 0, 0)
+    # maxQ = 0 / maxP = 0 bound only the neighbourhood, not the first candidates (:325-327, :369-370)
+    tr3 = []
+    O.autofit(sampled, 0, 2, 0, trace=tr3)
+    assert tr3[0] == [(0, 0, 1), (2, 2, 1), (1, 0, 1), (0, 1, 1)] and all(c[0] == 0 and c[1] == 0 for rnd in tr3[1:]
+                                                                          for c in rnd)
