@@ -61,13 +61,17 @@ extern "C" {
 /* ARIMA.autoFit outcomes (ARIMA.scala:280-375), arima_autofit_batch* only */
 #define ARIMA_ST_NOT_STATIONARY     11  /* no d <= max_d passes the KPSS test: "stationarity not achieved", :293-296 */
 #define ARIMA_ST_NO_MODEL           12  /* no candidate qualified: curBestModel stays null (NullPointerException)  */
-#define ARIMA_ST_CGD_FALLBACK       13  /* result returned, but a css-cgd candidate failed in the optimizer where the
-                                           reference retries with css-bobyqa (:315-319; not built): the selection
-                                           treats that retry as failed too, so it may differ from the reference's  */
+#define ARIMA_ST_FALLBACK_UNPINNED  13  /* result returned, but a candidate's css-bobyqa retry (fitTryBothStrategies,
+                                           :315-319) reached BOBYQA's RESCUE branch, which is not restated: that
+                                           candidate counts as failed, so the selection is unpinned                */
+/* css-bobyqa outcomes (ARIMA.fitWithCSSBOBYQA, ARIMA.scala:130-160) */
+#define ARIMA_ST_TOO_FEW_PARAMS     14  /* BOBYQAOptimizer needs >= 2 parameters (NumberIsTooSmallException)    */
+#define ARIMA_ST_BOBYQA_RESCUE      15  /* BOBYQA reached Powell's RESCUE branch (damaged denominator), which this
+                                           build does not restate: the fit stops there, outcome unpinned          */
 
 /* ---- fit methods (ARIMA.scala:105-109) -------------------------------------------------------------- */
 #define ARIMA_METHOD_CSS_CGD     0
-#define ARIMA_METHOD_CSS_BOBYQA  1      /* recognised, not implemented: series status ARIMA_ST_UNSUPPORTED_METHOD */
+#define ARIMA_METHOD_CSS_BOBYQA  1      /* commons BOBYQAOptimizer as ARIMA.fitWithCSSBOBYQA configures it (ARIMA.scala:130-160) */
 
 /* ---- stationarity / invertibility flags (ARIMAModel.isStationary / isInvertible, ARIMA.scala:777-815) - */
 #define ARIMA_FLAG_STATIONARY  1u
@@ -209,11 +213,12 @@ int arima_order_search_batch_device(arima_handle *h, const double *d_series, int
 /* ---- ARIMA.autoFit over a batch (ARIMA.scala:280-375; python/sparkts/models/ARIMA.py:25-60 `autofit`) --------- *
  * Per series: d = the first of 0..max_d whose differencesOfOrderD(ts, d) (NOT dropped) passes kpsstest(_, "c") at 5 %
  * (TimeSeriesStatisticalTests.scala:369-395); then findBestARMAModel's stepwise walk over (p, q, intercept) on that
- * differenced series with css-cgd fits (intercept only for d <= 1; the neighbourhood never changes q -- the
+ * differenced series with css-cgd fits, a css-bobyqa retry where css-cgd throws in the optimizer (fitTryBothStrategies,
+ * ARIMA.scala:315-319) (intercept only for d <= 1; the neighbourhood never changes q -- the
  * reference's quirks, ARIMA.scala:298-300, :356-366), keeping the first minimum approxAIC among stationary and
  * invertible fits. max_p, max_q <= 5. order_out N x 4 = (p, d, q, intercept) (-1s when the series has no model),
  * coef_out N x 11 (zero-padded; NaN when none), aic_out N (+inf when none), status_out N: ARIMA_ST_OK,
- * ARIMA_ST_CGD_FALLBACK (result valid, see above), ARIMA_ST_NOT_STATIONARY, ARIMA_ST_NO_MODEL, or the KPSS
+ * ARIMA_ST_FALLBACK_UNPINNED (result valid, see above), ARIMA_ST_NOT_STATIONARY, ARIMA_ST_NO_MODEL, or the KPSS
  * regression's shape status (T <= 1). n_fits_out (nullable): candidate fits the walk ran for the series.        */
 int arima_autofit_batch(arima_handle *h, const double *series, int64_t n_series, int32_t T, int32_t max_p,
                         int32_t max_d, int32_t max_q, int32_t *order_out, double *coef_out, double *aic_out,

@@ -48,6 +48,8 @@
 #define ORC_BRACKET_MAX 500    /* BracketFinder() = BracketFinder(100, 500) */
 #define ORC_KMAX 64
 
+int orc_bobyqa(const double *y, int len, int p, int q, int I, const double *x0, double *x_out, int *n_eval_out);
+
 /* ===================================================================================================== */
 /* fdlibm __ieee754_log (e_log.c), the algorithm behind java.lang.StrictMath.log                           */
 /* ===================================================================================================== */
@@ -695,6 +697,16 @@ int orc_fit(const double *ts, int T, int p, int d, int q, int I, int method, con
         if (st != ARIMA_ST_OK) { free(tmp); return st; }
     } else {
         memcpy(init, user_init, sizeof(double) * (size_t)k);
+    }
+    if (method == ARIMA_METHOD_CSS_BOBYQA) {                      /* :106 fitWithCSSBOBYQA, :130-160 */
+        double pt[ORC_KMAX];
+        st = orc_bobyqa(y, n, p, q, I, init, pt, &counters[0]);
+        if (st == ARIMA_ST_OK) {
+            memcpy(coef_out, pt, sizeof(double) * (size_t)k);
+            *ll_out = orc_loglik_css_arma(y, n, p, q, I, coef_out);
+        }
+        free(tmp);
+        return st;
     }
     if (method != ARIMA_METHOD_CSS_CGD) { free(tmp); return ARIMA_ST_UNSUPPORTED_METHOD; }  /* :105-109 */
     if (k == 0) { free(tmp); return ARIMA_ST_ZERO_PARAMS; }

@@ -68,7 +68,7 @@ struct AfSeries {                  // one series' walk state (findBestARMAModel'
     int32_t status;                // ARIMA_ST_*
     int32_t best;                  // packed p | q << 4 | I << 8 of curBestModel, -1 = null
     int32_t n_fits;                // candidate fits run so far
-    int32_t fallback;              // a css-cgd candidate threw where the reference tries css-bobyqa
+    int32_t fallback;              // a css-bobyqa retry reached the unrestated RESCUE branch
     int32_t ncand;                 // candidates of the current round (0: the walk is over)
     int32_t cand[kAfMaxCand];      // nextParams, packed, deduplicated in first-appearance order
     int32_t slot[kAfMaxCand];      // each candidate's row in its order's list this round
@@ -87,6 +87,13 @@ int launch_af_update(int64_t N, AfSeries *st, const int64_t *off, const double *
                      hipStream_t s);
 int launch_af_finish(int64_t N, const AfSeries *st, const double *best_coef, int32_t *order_out, double *coef_out,
                      double *aic_out, int32_t *status_out, int32_t *n_fits_out, hipStream_t s);
+
+// css-bobyqa (arima_bobyqa.hip): one lane per series after the initial parameters; refit_status (optional): only the
+// series whose css-cgd status there is an optimizer exception (autoFit's fitTryBothStrategies) are refitted in place
+int launch_bobyqa_fit(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, const double *init,
+                      const int32_t *init_status, const int32_t *refit_status, double *coef_out, double *ll_out,
+                      int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
+                      hipStream_t s);
 
 int hr_shape_status_host(int n, int p, int q, int I);
 int ar_shape_status_host(int n, int p, int I);

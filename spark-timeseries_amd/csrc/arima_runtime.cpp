@@ -147,6 +147,13 @@ struct arima_handle {
     int64_t last_grid = 0;
     int search_lanes = 8;          // concurrent fits of the order search (2/4/8: 1269/1303/1408 series/s, profiles/r02/g_c5)
     int pipeline = 1;              // fit contexts in rotation (option "fit_pipeline")
+    // one device fit call cut into this many slices on as many fit contexts (option "call_slices"; 1 = off, the
+    // default; -1 = auto: 3 for a call of >= 3 x call_slice_min series at fit_pipeline 1 on the handle's own streams).
+    // The slices of ONE call overlap while calls stay ordered (the next call waits for every slice). Measured on the
+    // box's 4 hardware queues at C2 1M x 1024 (profiles/r05/c_af2/default_cs*.json): 1 / 2 / 3 / 4 slices 6.91 /
+    // 6.39 / 6.35 / 4.47 M series/s -- every slice ends with its own slowest series, so it stays off
+    int call_slices = 1;
+    int64_t call_slice_min = 262144;
     int host_pipeline = 3;         // contexts the chunked host path rotates over
     int64_t host_chunk = 1 << 18;  // series per chunk of the host path (option "host_chunk")
     int64_t fit_slice_bytes = 0;   // differenced workspace of one device-fit slice (option "fit_slice_bytes"; 0: from free HBM)
@@ -292,6 +299,11 @@ const char *arima_status_name(int s) {
     case ARIMA_ST_ZERO_PARAMS: return "ZERO_PARAMS";
     case ARIMA_ST_UNSUPPORTED_METHOD: return "UNSUPPORTED_METHOD";
     case ARIMA_ST_SERIES_TOO_SHORT: return "SERIES_TOO_SHORT";
+    case ARIMA_ST_NOT_STATIONARY: return "NOT_STATIONARY";
+    case ARIMA_ST_NO_MODEL: return "NO_MODEL";
+    case ARIMA_ST_FALLBACK_UNPINNED: return "FALLBACK_UNPINNED";
+    case ARIMA_ST_TOO_FEW_PARAMS: return "TOO_FEW_PARAMS";
+    case ARIMA_ST_BOBYQA_RESCUE: return "BOBYQA_RESCUE";
     default: return "UNKNOWN";
     }
 }
@@ -518,6 +530,11 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
         h->search_lanes = (int)std::min<int64_t>(kMaxSearchLanes, std::max<int64_t>(1, value));
         return ARIMA_OK;
     }
+    if (!strcmp(name, "call_slices")) {
+        h->call_slices = (int)std::min<int64_t>(kMaxPipeline, std::max<int64_t>(-1, value));
+        return ARIMA_OK;
+    }
+    if (!strcmp(name, "call_slice_min")) { h->call_slice_min = std::max<int64_t>(1024, value); return ARIMA_OK; }
     if (!strcmp(name, "fit_pipeline")) {
         h->pipeline = (int)std::min<int64_t>(kMaxPipeline, std::max<int64_t>(1, value));
         return ARIMA_OK;
@@ -541,6 +558,7 @@ int arima_get_option(const arima_handle *hc, const char *name, int64_t *value) {
         {"host_chunk", h->host_chunk}, {"fit_slice_bytes", h->fit_slice_bytes}, {"express_ring", h->express_ring},
         {"hr_grid", h->hr_grid}, {"row_pad", h->row_pad}, {"merge_live", h->merge_live},
         {"search_express_blocks", h->search_express_blocks}, {"donate_evals", h->donate_evals},
+        {"call_slices", h->call_slices}, {"call_slice_min", h->call_slice_min},
         {"donate_evals_drained", h->donate_evals_drained}};
     for (const auto &o : opts)
         if (!strcmp(name, o.n)) {
@@ -620,6 +638,11 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
         init_status = ws.hr_status.as<int32_t>();
     }
     if (ev_mid) HIPCHK(h, hipEventRecord(ev_mid, s));
+    if (method == ARIMA_METHOD_CSS_BOBYQA && k > 0) {           // fitWithCSSBOBYQA, ARIMA.scala:106, :130-160
+        RCCHK(h, sts::launch_bobyqa_fit(y, ldn, n, N, p, q, I, init, init_status, nullptr, d_coef, d_ll, d_status,
+                                        d_neval, d_ngrad, d_flags, s), "bobyqa_fit");
+        return ARIMA_OK;
+    }
     if (method != ARIMA_METHOD_CSS_CGD || k == 0) {
         const unsigned grid = (unsigned)((N + 255) / 256);
         const int32_t code = (method != ARIMA_METHOD_CSS_CGD) ? ARIMA_ST_UNSUPPORTED_METHOD : ARIMA_ST_ZERO_PARAMS;
@@ -828,7 +851,16 @@ int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_se
         for (int j = 0; j < P; ++j) held += h->fctx[j].diff.bytes;
         slice_bytes = std::max<int64_t>(1ll << 30, (int64_t)((free_b + held) / 10 * 6 / (size_t)std::max(P, 1)));
     }
-    const int64_t slice = std::max<int64_t>(1024, slice_bytes / (ldn * (int64_t)sizeof(double)) / 1024 * 1024);
+    int64_t slice = std::max<int64_t>(1024, slice_bytes / (ldn * (int64_t)sizeof(double)) / 1024 * 1024);
+    // call slicing (fit_pipeline 1, the handle's streams): S slices of one call on S contexts
+    int S = 1;
+    if (P == 1 && !stream && n_series > 0) {
+        S = h->call_slices >= 2 ? h->call_slices
+                                : (h->call_slices < 0 && n_series >= 3 * h->call_slice_min ? 3 : 1);
+        S = std::min(S, kMaxPipeline);
+        if (S > 1) slice = std::min(slice, std::max<int64_t>(1024, (n_series + S - 1) / S));
+    }
+    const int PC = std::max(P, S);                 // contexts this call's slices rotate over
     if (n_series <= slice || T < 0 || ld < T || n_series < 0) {
         const int ci = (int)(h->fit_seq++ % (unsigned)P);
         FitCtx &c = h->fctx[ci];
@@ -850,6 +882,10 @@ int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_se
     h->slice_first = h->slot_seq % kSliceSlots;
     h->slice_n = 0;
     h->slice_acc = arima_fit_stats{};
+    if (P == 1 && PC > 1 && !stream && h->fctx[0].has_done)
+        // calls stay ordered: every context of this call starts after the previous fit call (whose end context 0's
+        // event marks at fit_pipeline 1), captured before slice 0 re-records that event
+        for (int j = 1; j < PC; ++j) HIPCHK(h, hipStreamWaitEvent(h->fctx[j].stream, h->fctx[0].ev_done, 0));
     for (int64_t j = 0; j < nslices; ++j) {
         const int sl = (int)(h->slot_seq++ % kSliceSlots);
         SliceSlot &ss = h->slot[sl];
@@ -868,18 +904,26 @@ int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_se
         }
         ss.ps = PendingStats{};
         const int64_t f = j * slice, ns = std::min(slice, n_series - f);
-        const int ci = (int)(h->fit_seq++ % (unsigned)P);
+        // fit_pipeline P > 1: the next context in the rotation; call slicing at P = 1: context j % S
+        const int ci = P > 1 ? (int)(h->fit_seq++ % (unsigned)P) : (int)(j % PC);
         FitCtx &c = h->fctx[ci];
         hipStream_t s = stream ? (hipStream_t)stream : c.stream;
         begin_fit(h, c, s);
         const int rc = fit_device_locked(
-            h, c, ci, P, d_series + f * ld, ns, T, ld, p, d, q, include_intercept, method,
+            h, c, ci, PC, d_series + f * ld, ns, T, ld, p, d, q, include_intercept, method,
             d_user_init ? d_user_init + f * k : nullptr, d_coef_out + f * k, d_css_ll_out + f, d_status_out + f,
             d_n_eval_out ? d_n_eval_out + f : nullptr, d_n_grad_out ? d_n_grad_out + f : nullptr,
-            d_flags_out ? d_flags_out + f : nullptr, s, P > 1, sl);
+            d_flags_out ? d_flags_out + f : nullptr, s, PC > 1, sl);
         HIPCHK(h, end_fit(c, s));
         h->slice_n++;
         if (rc != ARIMA_OK) return rc;
+    }
+    if (P == 1 && PC > 1) {
+        // the call ends when every slice has: context 0 (the next call's, at fit_pipeline 1) waits for all of them
+        FitCtx &c0 = h->fctx[0];
+        for (int j = 1; j < PC; ++j)
+            if (h->fctx[j].has_done) HIPCHK(h, hipStreamWaitEvent(c0.stream, h->fctx[j].ev_done, 0));
+        HIPCHK(h, end_fit(c0, c0.stream));
     }
     return ARIMA_OK;
 }
@@ -1610,6 +1654,14 @@ static int autofit_locked(arima_handle *h, const double *d_series, int64_t N, in
                                  h->af_coef.as<double>() + off[cb] * 11, h->af_ll.as<double>() + off[cb],
                                  h->af_status.as<int32_t>() + off[cb], nullptr, nullptr,
                                  h->af_flags.as<uint8_t>() + off[cb], c.stream, nullptr, &gridb, &xb, P > 1), "fit");
+            // fitTryBothStrategies (:315-319): the series whose css-cgd fit threw in the optimizer, refitted with
+            // css-bobyqa from the same Hannan-Rissanen init, in place (the AR-only shortcut never reaches a method)
+            if (!(p > 0 && q == 0))
+                RCCHK(h, sts::launch_bobyqa_fit(c.diff.as<double>(), ldT, T, cnt, p, q, I, c.ws.init.as<double>(),
+                                                c.ws.hr_status.as<int32_t>(), h->af_status.as<int32_t>() + off[cb],
+                                                h->af_coef.as<double>() + off[cb] * 11, h->af_ll.as<double>() + off[cb],
+                                                h->af_status.as<int32_t>() + off[cb], nullptr, nullptr,
+                                                h->af_flags.as<uint8_t>() + off[cb], c.stream), "bobyqa refit");
             HIPCHK(h, end_fit(c, c.stream));
             ++used;
         }

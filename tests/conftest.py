@@ -26,7 +26,10 @@ def load_case(name):
 
 
 def all_cases(prefix=""):
-    return sorted(os.path.basename(f)[:-4] for f in glob.glob(os.path.join(GOLDEN, prefix + "*.npz")))
+    """Golden fit fixtures (prefix ""), or those of a prefix; the autoFit fixtures (autofit_*) hold another layout
+    and are only listed when asked for by their prefix."""
+    names = sorted(os.path.basename(f)[:-4] for f in glob.glob(os.path.join(GOLDEN, prefix + "*.npz")))
+    return names if prefix.startswith("autofit") else [n for n in names if not n.startswith("autofit_")]
 
 
 @pytest.fixture(scope="session")

@@ -108,7 +108,7 @@ def main():
     nanser[1, 0] = np.nan
     nanser[2, :] = np.inf
     run_case("edge_nan_101", nanser, 1, 0, 1, 1)
-    run_case("edge_unsupported_method", ds1, 1, 0, 1, 1, method=1)
+    run_case("edge_unsupported_method", ds1, 1, 0, 1, 1, method=99)             # an unknown method string
     run_case("edge_userinit_nonfinite", ds1, 1, 0, 1, 1, user_init=[np.nan, 0.2, 1.0])
     run_case("edge_userinit_wild", ds1, 1, 0, 1, 1, user_init=[0.0, 3.0, -4.0])
 

@@ -125,6 +125,21 @@ int main() {
         for (double &v : ts) v *= 1e150;
         check_series(ts, o[0], o[1], o[2], o[3], 1, "huge");
     }
+    // css-bobyqa (oracle/bobyqa_oracle.c): every array of Powell's routines under the sanitizers, over the orders,
+    // short and edge series (its results are checked against the device by tests/test_gpu_bobyqa.py)
+    for (const auto &o : orders)
+        for (int T : {0, 3, 9, 16, 40, 300}) {
+            std::vector<double> ts = arima_series(T, o[0], o[1], o[2], o[3]);
+            double coef[16], ll;
+            int cnt[3];
+            orc_fit(ts.empty() ? nullptr : ts.data(), T, o[0], o[1], o[2], o[3], 1, nullptr, 1, coef, &ll, cnt);
+            std::vector<double> flat(T > 0 ? T : 1, 3.25), nan_ts = ts;
+            orc_fit(T ? flat.data() : nullptr, T, o[0], o[1], o[2], o[3], 1, nullptr, 1, coef, &ll, cnt);
+            if (T > 20) {
+                nan_ts[T / 2] = NAN;
+                orc_fit(nan_ts.data(), T, o[0], o[1], o[2], o[3], 1, nullptr, 1, coef, &ll, cnt);
+            }
+        }
     // building blocks the fit does not reach on its own
     for (const auto &o : orders) {
         const int p = o[0], d = o[1], q = o[2], I = o[3], k = I + p + q;

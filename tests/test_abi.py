@@ -45,9 +45,10 @@ def test_pure_host_entry_points():
     import sparkts_amd._lib as L
     lib = L.load()
     assert lib.arima_num_params(2, 2, 1) == 5 and lib.arima_num_params(0, 0, 0) == 0
-    names = [lib.arima_status_name(i).decode() for i in range(11)]
+    names = [lib.arima_status_name(i).decode() for i in range(16)]
     assert names == ["OK", "MAX_EVAL", "BRACKET_MAX_EVAL", "MAX_ITER", "SINGULAR", "NOT_ENOUGH_DATA", "NO_DATA",
-                     "BAD_INTERVAL", "ZERO_PARAMS", "UNSUPPORTED_METHOD", "SERIES_TOO_SHORT"]
+                     "BAD_INTERVAL", "ZERO_PARAMS", "UNSUPPORTED_METHOD", "SERIES_TOO_SHORT", "NOT_STATIONARY",
+                     "NO_MODEL", "FALLBACK_UNPINNED", "TOO_FEW_PARAMS", "BOBYQA_RESCUE"]
 
 
 def test_status_codes_match_oracle_numbering():

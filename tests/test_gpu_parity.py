@@ -35,11 +35,13 @@ def check_fit(res, exp, ctx):
     assert np.array_equal(res["n_grad"], exp["n_grad"]), f"{ctx}: n_grad"
     if ok.any():
         c, ce = res["coef"][ok], exp["coef"][ok]
-        assert np.all(np.abs(c - ce) <= COEF_ATOL), f"{ctx}: coef tolerance"
+        fin = np.isfinite(ce)                  # a normal return can sit at a NaN point (css-bobyqa on NaN models)
+        assert np.all(np.abs(c - ce)[fin] <= COEF_ATOL), f"{ctx}: coef tolerance"
         ll, lle = res["ll"][ok], exp["ll"][ok]
-        assert np.all(np.abs(ll - lle) <= LL_RTOL * np.abs(lle)), f"{ctx}: LL tolerance"
-        assert np.array_equal(c, ce), f"{ctx}: coefficients not bit-identical: max diff {np.max(np.abs(c - ce))}"
-        assert np.array_equal(ll, lle), f"{ctx}: LL not bit-identical"
+        lf = np.isfinite(lle)
+        assert np.all(np.abs(ll - lle)[lf] <= LL_RTOL * np.abs(lle)[lf]), f"{ctx}: LL tolerance"
+        assert _same(c, ce), f"{ctx}: coefficients not bit-identical: max diff {np.nanmax(np.abs(c - ce))}"
+        assert _same(ll, lle), f"{ctx}: LL not bit-identical"
         assert np.array_equal(res["flags"][ok], exp["flags"][ok]), f"{ctx}: flags"
     assert np.all(np.isnan(res["coef"][~ok])), f"{ctx}: failed fits must report NaN coefficients"
 
@@ -191,7 +193,10 @@ def test_python_mirror_api(engine):
     assert m.is_stationary() and m.is_invertible()
     assert m.approx_aic(arr["series"][0]) == -2 * arr["ll"][0] + 2 * 3
     with pytest.raises(ARIMA.UnsupportedOperationException):
-        ARIMA.fit_model(1, 0, 1, arr["series"][0], method="css-bobyqa")
+        ARIMA.fit_model(1, 0, 1, arr["series"][0], method="css-newton")
+    mb = ARIMA.fit_model(1, 0, 1, arr["series"][0], method="css-bobyqa")
+    eb = O.fit(arr["series"][0], 1, 0, 1, method=1)
+    assert np.array_equal(mb.coefficients, eb["coef"])
     with pytest.raises(ARIMA.TooManyEvaluationsException):
         ARIMA.fit_model(1, 0, 1, np.full(50, np.nan))
     from sparkts_amd import fit_arima_partition

@@ -160,7 +160,7 @@ def test_status_semantics():
     # ARIMA(0,0,0) without intercept: OLS with zero columns -> NoDataException
     assert O.fit(np.arange(30.0), 0, 0, 0, intercept=False)["status"] == 6
     # unknown method after a successful HR init -> UnsupportedOperationException
-    assert O.fit(DS1, 1, 0, 1, method=1)["status"] == 9
+    assert O.fit(DS1, 1, 0, 1, method=99)["status"] == 9
 
 
 KPSS_R_V = [0.0187461709418264, -0.184252542069064, -1.37133054992251, -0.599167715783718,
@@ -224,3 +224,37 @@ def test_autofit_walk_quirks():
     O.autofit(sampled, 0, 2, 0, trace=tr3)
     assert tr3[0] == [(0, 0, 1), (2, 2, 1), (1, 0, 1), (0, 1, 1)] and all(c[0] == 0 and c[1] == 0 for rnd in tr3[1:]
                                                                           for c in rnd)
+
+
+@pytest.mark.parametrize("name", ["autofit_kat_maxd2", "autofit_kat_maxd10", "autofit_mixed_T256_p2q1"])
+def test_autofit_fixtures_match_the_oracle(name):
+    # the committed autoFit vectors (tests/golden/make_golden_autofit.py) are the current restatement's outputs
+    from conftest import load_case
+    meta, arr = load_case(name)
+    for i, row in enumerate(arr["series"]):
+        r = O.autofit(row, meta["max_p"], meta["max_d"], meta["max_q"])
+        assert r["status"] == arr["status"][i] and tuple(r["order"]) == tuple(arr["order"][i])
+        assert r["n_fits"] == arr["n_fits"][i]
+        assert np.array_equal(r["coef"], arr["coef"][i], equal_nan=True) and (r["aic"] == arr["aic"][i])
+
+
+def test_bobyqa_similar_to_cgd_kat():
+    # ARIMASuite.scala:58-74: ARIMAModel(2,1,2,[8.2,0.2,0.5,0.3,0.1]).sample(1000, MersenneTwister(10)) fitted with
+    # css-bobyqa and css-cgd: intercepts within 1, the other coefficients within 0.1
+    s = O.add_time_dependent_effects(mt_gauss(10, 1000), 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1])
+    b = O.fit(s, 2, 1, 2, method=1)
+    c = O.fit(s, 2, 1, 2)
+    assert b["status"] == 0 and c["status"] == 0 and b["n_grad"] == 0 and b["n_eval"] > 2 * 5 + 1
+    assert abs(b["coef"][0] - c["coef"][0]) < 1
+    assert np.all(np.abs(b["coef"][1:] - c["coef"][1:]) < 0.1)
+    # BOBYQA maximises the same objective: it ends at least as high as the CG fit's loose stopping point here
+    assert b["ll"] >= c["ll"]
+
+
+def test_bobyqa_status_semantics():
+    # BOBYQAOptimizer.setup: dimension >= 2 (NumberIsTooSmallException) -- after the Hannan-Rissanen init
+    assert O.fit(DS1, 0, 0, 1, intercept=False, method=1)["status"] == 14
+    assert O.fit(DS1, 0, 0, 0, intercept=False, method=1)["status"] == 6          # HR throws first (NoData)
+    assert O.fit(DS1, 2, 0, 0, method=1)["status"] == 0                           # AR-only shortcut, no method
+    r = O.fit(DS1, 1, 0, 1, method=1, user_init=[0.0, 0.2, 1.0])
+    assert r["status"] == 0 and abs(r["coef"][1] - 0.3) < 0.05 and abs(r["coef"][2] - 0.7) < 0.05
