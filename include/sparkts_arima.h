@@ -56,7 +56,7 @@ extern "C" {
 #define ARIMA_ST_NO_DATA             6  /* NoDataException: zero rows, or zero columns without intercept     */
 #define ARIMA_ST_BAD_INTERVAL        7  /* NumberIsTooLarge / OutOfRange from SearchInterval (line search)   */
 #define ARIMA_ST_ZERO_PARAMS         8  /* k == 0 parameters (ArithmeticException / index error)             */
-#define ARIMA_ST_UNSUPPORTED_METHOD  9  /* UnsupportedOperationException, ARIMA.scala:108 (and css-bobyqa)   */
+#define ARIMA_ST_UNSUPPORTED_METHOD  9  /* UnsupportedOperationException, ARIMA.scala:108 (unknown method)    */
 #define ARIMA_ST_SERIES_TOO_SHORT   10  /* negative lag-matrix size (NegativeArraySize / IndexOutOfBounds)    */
 /* ARIMA.autoFit outcomes (ARIMA.scala:280-375), arima_autofit_batch* only */
 #define ARIMA_ST_NOT_STATIONARY     11  /* no d <= max_d passes the KPSS test: "stationarity not achieved", :293-296 */

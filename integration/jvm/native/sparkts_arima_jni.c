@@ -73,3 +73,14 @@ JNIEXPORT jint JNICALL JNI_FN(orderSearch)(JNIEnv *env, jobject self, jlong h, j
                                     maxD, maxQ, interceptMode, method, (int32_t *)BUF(env, order),
                                     (double *)BUF(env, coef), (double *)BUF(env, aic));
 }
+
+/* arima_autofit_batch (ARIMA.autoFit, ARIMA.scala:280-375): series N x T, order N x 4, coef N x 11, aic / status /
+ * n_fits N */
+JNIEXPORT jint JNICALL JNI_FN(autoFit)(JNIEnv *env, jobject self, jlong h, jobject series, jlong n, jint t, jint maxP,
+                                       jint maxD, jint maxQ, jobject order, jobject coef, jobject aic, jobject status,
+                                       jobject nFits) {
+    (void)self;
+    return arima_autofit_batch((arima_handle *)(intptr_t)h, (const double *)BUF(env, series), n, t, maxP, maxD,
+                               maxQ, (int32_t *)BUF(env, order), (double *)BUF(env, coef), (double *)BUF(env, aic),
+                               (int32_t *)BUF(env, status), (int32_t *)BUF(env, nFits));
+}

@@ -11,6 +11,9 @@
  *                                              JavaTimeSeriesRDD.scala:124-133), batched per partition
  *   ArimaMI355X.forecastMany / orderSearchMany batched ARIMAModel.forecast (ARIMA.scala:696-764) and the
  *                                              min-approxAIC order grid (ARIMA.scala:280-375, 826-830)
+ *   ArimaMI355X.autoFit / autoFitMany          drop-in for ARIMA.autoFit (ARIMA.scala:280-375): KPSS choice of d,
+ *                                              stepwise walk with the css-bobyqa retry, batched per partition
+ *   method = "css-bobyqa"                      fitWithCSSBOBYQA (ARIMA.scala:130-160) on the device
  */
 package com.cloudera.sparkts.models
 
@@ -39,6 +42,9 @@ object ArimaMI355XNative {
   @native def orderSearch(handle: Long, series: DoubleBuffer, n: Long, t: Int, maxP: Int, maxD: Int, maxQ: Int,
                           interceptMode: Int, method: Int, order: IntBuffer, coef: DoubleBuffer,
                           aic: DoubleBuffer): Int
+  @native def autoFit(handle: Long, series: DoubleBuffer, n: Long, t: Int, maxP: Int, maxD: Int, maxQ: Int,
+                      order: IntBuffer, coef: DoubleBuffer, aic: DoubleBuffer, status: IntBuffer,
+                      nFits: IntBuffer): Int
 }
 
 /** Per-series status codes of include/sparkts_arima.h, mapped back to the exception the reference throws. */
@@ -46,6 +52,8 @@ object ArimaStatus {
   val OK = 0; val MAX_EVAL = 1; val BRACKET_MAX_EVAL = 2; val MAX_ITER = 3; val SINGULAR = 4
   val NOT_ENOUGH_DATA = 5; val NO_DATA = 6; val BAD_INTERVAL = 7; val ZERO_PARAMS = 8
   val UNSUPPORTED_METHOD = 9; val SERIES_TOO_SHORT = 10
+  val NOT_STATIONARY = 11; val NO_MODEL = 12; val FALLBACK_UNPINNED = 13; val TOO_FEW_PARAMS = 14
+  val BOBYQA_RESCUE = 15
 
   def toException(status: Int): Throwable = status match {
     case MAX_EVAL => new TooManyEvaluationsException(10000)                    // MaxEval(10000), ARIMA.scala:196
@@ -58,6 +66,11 @@ object ArimaStatus {
     case ZERO_PARAMS => new ArithmeticException("/ by zero")
     case UNSUPPORTED_METHOD => new UnsupportedOperationException()             // ARIMA.scala:108
     case SERIES_TOO_SHORT => new IndexOutOfBoundsException()
+    case NOT_STATIONARY => new Exception("stationarity not achieved with differencing order <= maxD")  // :295
+    case NO_MODEL => new NullPointerException()                                // curBestModel == null, :302
+    case TOO_FEW_PARAMS => new org.apache.commons.math3.exception.NumberIsTooSmallException(1: Integer, 2: Integer, true)
+    case BOBYQA_RESCUE | FALLBACK_UNPINNED =>
+      new IllegalStateException("BOBYQA's RESCUE branch is not restated by the MI355X engine")
     case other => new IllegalStateException(s"unknown ARIMA status $other")
   }
 }
@@ -73,7 +86,7 @@ object ArimaMI355X {
 
   private def methodCode(method: String): Int = method match {
     case "css-cgd" => 0
-    case "css-bobyqa" => 1                                        // recognised; per-series UNSUPPORTED_METHOD
+    case "css-bobyqa" => 1                                        // fitWithCSSBOBYQA, ARIMA.scala:130-160
     case _ => 99                                                  // -> UNSUPPORTED_METHOD, as ARIMA.scala:108
   }
 
@@ -163,6 +176,34 @@ object ArimaMI355X {
   /** The min-approxAIC (ARIMA.scala:826-830) model per series over d <= maxD, p <= maxP, q <= maxQ and the
     * intercept modes, among fits that returned normally and are stationary and invertible (ARIMA.scala:342).
     * Returns (p, d, q, intercept) per series (-1s when nothing qualified), coefficients and AIC. */
+  /** Drop-in for ARIMA.autoFit (ARIMA.scala:280-304): one series, the reference's exceptions. */
+  def autoFit(ts: Vector, maxP: Int = 5, maxD: Int = 2, maxQ: Int = 5): ARIMAModel = {
+    val (order, coef, _, status) = autoFitMany(Array(ts.toArray), maxP, maxD, maxQ)
+    if (status(0) != ArimaStatus.OK) throw ArimaStatus.toException(status(0))
+    val Array(p, d, q, c) = order(0)
+    new ARIMAModel(p, d, q, coef(0).take(p + q + c), c == 1)
+  }
+
+  /** Batched ARIMA.autoFit: (p, d, q, intercept), coefficients (11, zero-padded), approxAIC and status per series. */
+  def autoFitMany(values: Array[Array[Double]], maxP: Int = 5, maxD: Int = 2, maxQ: Int = 5)
+      : (Array[Array[Int]], Array[Array[Double]], Array[Double], Array[Int]) = {
+    val n = values.length
+    val t = if (n == 0) 0 else values(0).length
+    val series = doubles(n.toLong * t)
+    values.foreach(v => series.put(v))
+    series.flip()
+    val order = ints(math.max(4L * n, 1L))
+    val coef = doubles(math.max(11L * n, 1L))
+    val aic = doubles(math.max(n, 1))
+    val status = ints(math.max(n, 1))
+    val nFits = ints(math.max(n, 1))
+    check(ArimaMI355XNative.autoFit(handle, series, n, t, maxP, maxD, maxQ, order, coef, aic, status, nFits),
+      "arima_autofit_batch")
+    (Array.tabulate(n)(i => Array.tabulate(4)(j => order.get(4 * i + j))),
+      Array.tabulate(n)(i => Array.tabulate(11)(j => coef.get(11 * i + j))), Array.tabulate(n)(aic.get),
+      Array.tabulate(n)(status.get))
+  }
+
   def orderSearchMany(values: Array[Array[Double]], maxP: Int = 5, maxD: Int = 2, maxQ: Int = 5,
                       interceptMode: Int = 2): (Array[Array[Int]], Array[Array[Double]], Array[Double]) = {
     val n = values.length

@@ -12,14 +12,14 @@ OUT=${OUT:-gpurun_out}
 CFG=${CONFIG:-c2}
 mkdir -p $OUT
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_trace -o run --output-format csv -- \
-    python3 bench.py --config $CFG --series $SER --steps 2 --warmup 1 --cpu-seconds 0 --pipeline 1 --e2e 0 > $OUT/prof_bench.json 2> $OUT/prof_bench.err
+    python3 bench.py --config $CFG --series $SER --steps 2 --warmup 1 --cpu-seconds 0 --pipeline 1 --e2e 0 --default-leg 0 > $OUT/prof_bench.json 2> $OUT/prof_bench.err
 timeout -k 10 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $OUT/prof_fetch -o run --output-format csv -- \
-    python3 bench.py --config $CFG --series $SER --steps 1 --warmup 0 --cpu-seconds 0 --pipeline 1 --e2e 0 > /dev/null 2>&1
+    python3 bench.py --config $CFG --series $SER --steps 1 --warmup 0 --cpu-seconds 0 --pipeline 1 --e2e 0 --default-leg 0 > /dev/null 2>&1
 timeout -k 10 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $OUT/prof_write -o run --output-format csv -- \
-    python3 bench.py --config $CFG --series $SER --steps 1 --warmup 0 --cpu-seconds 0 --pipeline 1 --e2e 0 > /dev/null 2>&1
+    python3 bench.py --config $CFG --series $SER --steps 1 --warmup 0 --cpu-seconds 0 --pipeline 1 --e2e 0 --default-leg 0 > /dev/null 2>&1
 timeout -k 10 600 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES -d $OUT/prof_sq -o run --output-format csv -- \
-    python3 bench.py --config $CFG --series $SER --steps 1 --warmup 0 --cpu-seconds 0 --pipeline 1 --e2e 0 > /dev/null 2>&1
+    python3 bench.py --config $CFG --series $SER --steps 1 --warmup 0 --cpu-seconds 0 --pipeline 1 --e2e 0 --default-leg 0 > /dev/null 2>&1
 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM -d $OUT/prof_sqwait -o run --output-format csv -- \
-    python3 bench.py --config $CFG --series $SER --steps 1 --warmup 0 --cpu-seconds 0 --pipeline 1 --e2e 0 > /dev/null 2>&1
+    python3 bench.py --config $CFG --series $SER --steps 1 --warmup 0 --cpu-seconds 0 --pipeline 1 --e2e 0 --default-leg 0 > /dev/null 2>&1
 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum -d $OUT/prof_tcc -o run --output-format csv -- \
-    python3 bench.py --config $CFG --series $SER --steps 1 --warmup 0 --cpu-seconds 0 --pipeline 1 --e2e 0 > /dev/null 2>&1
+    python3 bench.py --config $CFG --series $SER --steps 1 --warmup 0 --cpu-seconds 0 --pipeline 1 --e2e 0 --default-leg 0 > /dev/null 2>&1
