@@ -62,7 +62,9 @@ CONFIGS = {
     "c1": (1, 0, 1, 1, 500, [3.5, 0.3, 0.7], 0.05),
     "c4": (5, 1, 5, 1, 4096, [0.1, 0.4, -0.2, 0.1, 0.05, -0.05, 0.3, 0.2, -0.1, 0.05, 0.05], 0.05),
 }
-DEFAULT_SERIES = {"c1": 10000}                 # configs[0]: 10k series; every other config 1M per GPU
+# configs[0]: 10k series; autoFit 64k (each of its ~7 rounds waits for its slowest css-bobyqa retry: 38 s per 64k
+# series, profiles/r05/j_css); every other config 1M per GPU
+DEFAULT_SERIES = {"c1": 10000, "af": 1 << 16}
 METRICS = {
     "c2": "series fitted/sec, ARIMA(2,1,2) CSS-CGD, 1M x 1024 pts",
     "c1": "series fitted/sec, ARIMA(1,0,1) CSS-CGD, 10k x 500 pts (BASELINE.json configs[0])",
@@ -121,6 +123,30 @@ def physical_cores():
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+class heartbeat:
+    """A line on stderr every `every` s while a long device call runs (a silent minute reads as a hang on the box);
+    ctypes releases the GIL during the call, so the thread gets to run."""
+
+    def __init__(self, what, every=30):
+        self.what, self.every = what, every
+
+    def __enter__(self):
+        import threading
+        self.done, t0 = threading.Event(), time.perf_counter()
+
+        def beat():
+            while not self.done.wait(self.every):
+                log(f"{self.what} ... {time.perf_counter() - t0:.0f} s")
+        self.th = threading.Thread(target=beat, daemon=True)
+        self.th.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.done.set()
+        self.th.join()
+        return False
 
 
 def _free_port():
@@ -213,7 +239,7 @@ def oracle_rows(series_host, p, d, q, I, smear, budget_s):
 
 def run_default_leg(args):
     """the drop-in as a caller gets it -- arima_fit_batch_device with the ABI's default options
-    (no arima_set_option call: fit_pipeline 1, the default scheduler knobs) under the box's own GPU_MAX_HW_QUEUES, in a
+    (no arima_set_option call: fit_pipeline 3, the default scheduler knobs) under the box's own GPU_MAX_HW_QUEUES, in a
     child process that runs to completion before this process touches the GPU. Returns its JSON line (or an error)."""
     env = dict(os.environ, SPARKTS_BENCH_DEFAULT_LEG="1")
     if _BOX_QUEUES is None:
@@ -245,11 +271,18 @@ def default_leg_child(args):
     eng = L.Engine.get(dev_id)                  # no set_option: the ABI's defaults
     series = torch.empty((N, T), dtype=torch.float64, device=dev)
     eng.sample_device(series.data_ptr(), N, T, T, p, d, q, I, base, jitter, SEED, 0)
-    o = dict(coef=torch.empty((N, k), dtype=torch.float64, device=dev), ll=torch.empty(N, dtype=torch.float64, device=dev),
-             status=torch.empty(N, dtype=torch.int32, device=dev), n_eval=torch.empty(N, dtype=torch.int32, device=dev),
-             n_grad=torch.empty(N, dtype=torch.int32, device=dev), flags=torch.empty(N, dtype=torch.uint8, device=dev))
+    # every call writes its own result buffers, as consecutive partitions of a mapSeries would (calls that share
+    # buffers would be ordered by the library: tests/test_gpu_parity.py::test_pipelined_fits_that_share_buffers_...)
+    outs = [dict(coef=torch.empty((N, k), dtype=torch.float64, device=dev),
+                 ll=torch.empty(N, dtype=torch.float64, device=dev), status=torch.empty(N, dtype=torch.int32, device=dev),
+                 n_eval=torch.empty(N, dtype=torch.int32, device=dev),
+                 n_grad=torch.empty(N, dtype=torch.int32, device=dev),
+                 flags=torch.empty(N, dtype=torch.uint8, device=dev)) for _ in range(args.warmup + args.steps)]
+    calls = [0]
 
     def step():
+        o = outs[calls[0] % len(outs)]
+        calls[0] += 1
         eng.fit_batch_device(series.data_ptr(), N, T, T, p, d, q, I, o["coef"].data_ptr(), o["ll"].data_ptr(),
                              o["status"].data_ptr(), o["n_eval"].data_ptr(), o["n_grad"].data_ptr(),
                              o["flags"].data_ptr(), blocking=False)
@@ -378,9 +411,9 @@ def main():
 
     p, d, q, I, T, base, jitter = CONFIGS[args.config]
     if args.steps is None:                  # enough steps that the pipeline's fill is amortised (C2: 3 steps read
-        args.steps = {"c4": 5, "c5": 2, "af": 3}.get(args.config, 20)   # 9.35 M series/s, 20 steps 11.0, profiles/r04/zz_check)
+        args.steps = {"c4": 5, "c5": 2, "af": 2}.get(args.config, 20)   # 9.35 M series/s, 20 steps 11.0, profiles/r04/zz_check)
     if args.warmup is None:
-        args.warmup = 1 if args.config == "c5" else 3
+        args.warmup = 1 if args.config in ("c5", "af") else 3
     if args.pipeline <= 0:
         args.pipeline = 4 if args.config == "c4" else 6
     if args.config == "c5" and not args.total_series:
@@ -639,23 +672,11 @@ def run_c5(args, eng, series, N, T, total_series, world, rank, dev, barrier, dis
     coef = torch.empty((max(N, 1), 11), dtype=torch.float64, device=dev)
     aic = torch.empty(max(N, 1), dtype=torch.float64, device=dev)
 
-    def step():
-        import threading
+    def step():                            # a full-size search runs for minutes
         eng.order_search_device(series.data_ptr(), N, T, T, 5, 2, 5, 2, order.data_ptr(), coef.data_ptr(),
                                 aic.data_ptr(), blocking=False)
-        done = threading.Event()
-        t0 = time.perf_counter()
-
-        def progress():                    # a full-size search runs for minutes: a line every 30 s
-            while not done.wait(30):
-                log(f"[rank {rank}] searching ... {time.perf_counter() - t0:.0f} s")
-        th = threading.Thread(target=progress, daemon=True)
-        th.start()
-        try:
+        with heartbeat(f"[rank {rank}] searching"):
             eng.synchronize()
-        finally:
-            done.set()
-            th.join()
 
     for i in range(args.warmup):
         step()
@@ -739,8 +760,10 @@ def run_af(args, eng, series, N, T, total_series, world, rank, dev, barrier, dis
                n_fits=torch.empty(max(N, 1), dtype=torch.int32, device=dev))
 
     def step():
-        eng.autofit_device(series.data_ptr(), N, T, T, 5, 2, 5, out["order"].data_ptr(), out["coef"].data_ptr(),
-                           out["aic"].data_ptr(), out["status"].data_ptr(), out["n_fits"].data_ptr(), blocking=True)
+        with heartbeat(f"[rank {rank}] auto-fitting"):
+            eng.autofit_device(series.data_ptr(), N, T, T, 5, 2, 5, out["order"].data_ptr(), out["coef"].data_ptr(),
+                               out["aic"].data_ptr(), out["status"].data_ptr(), out["n_fits"].data_ptr(),
+                               blocking=True)
     for _ in range(args.warmup):
         step()
     barrier()

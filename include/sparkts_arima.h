@@ -16,9 +16,10 @@
  *     `void*` (NULL = the handle's own stream) and are asynchronous w.r.t. the host: they enqueue their work
  *     and return (results are valid once that stream reaches the call's end). Calls on one handle are also
  *     ordered on the device whichever streams they use, because they share the handle's workspaces --
- *     except fit calls under the "fit_pipeline" option (arima_set_option): with fit_pipeline = P > 1,
- *     consecutive arima_fit_batch_device calls rotate over P fit contexts and may run concurrently (the
- *     caller must not feed one fit's outputs to a later fit before arima_synchronize). Every non-fit call
+ *     except fit calls under the "fit_pipeline" option (arima_set_option; default 3): consecutive
+ *     arima_fit_batch_device calls rotate over P fit contexts and may run concurrently -- unless a call's
+ *     buffers overlap an in-flight call's (it reads that call's outputs, writes its inputs, or writes the same
+ *     outputs): then it waits for that call, so results always equal fit_pipeline 1's. Every non-fit call
  *     still waits for all earlier calls. arima_get_last_stats waits for the last call's device work.
  *     Host-buffer entry points block (arima_fit_batch pipelines its own chunks internally: "host_chunk",
  *     "host_pipeline").
@@ -131,7 +132,7 @@ int         arima_get_last_stats(const arima_handle *h, arima_fit_stats *out);
 /* Blocks until the device work of every call issued on the handle so far has finished. */
 int         arima_synchronize(arima_handle *h);
 /* Tuning knobs (not part of the reference contract): "smear" (Breeze reading at ARIMA.scala:526, default 1),
- * "fit_pipeline" (fit contexts in rotation for *_device fits, 1..8, default 1), "host_chunk" / "host_pipeline"
+ * "fit_pipeline" (fit contexts in rotation for *_device fits, 1..8, default 3), "host_chunk" / "host_pipeline"
  * (series per chunk and contexts of the chunked host path, default 262144 / 3), "express_blocks",
  * "grid_blocks", "search_lanes" (in-kernel scheduler and order-search concurrency), "hr_grid" (k_hr_init grid:
  * 0 = a lane per series, > 0 = that

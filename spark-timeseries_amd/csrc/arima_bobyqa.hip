@@ -75,6 +75,37 @@ __device__ double bq_css_ll(const double *__restrict__ row, int n, int p, int q,
     return css_to_loglik(css, n);
 }
 
+// The same log-likelihood through css_pass (the css-cgd fits' objective pass: compile-time orders, the lag windows
+// in registers, no per-step moves), for the orders of dimension K = I + p + q; one lane, one chunk in flight
+template <int P, int Q, int I>
+__device__ __forceinline__ double bq_css_ll_t(const double *__restrict__ row, int n, const double *x) {
+    constexpr int KA = I + P + Q > 0 ? I + P + Q : 1;
+    double c[KA], g[KA], css;
+#pragma unroll
+    for (int j = 0; j < KA; ++j) c[j] = (j < I + P + Q) ? x[j] : 0.0;
+    css_pass<P, Q, I, false, true, 1>(row, n, c, css, g);
+    return css_to_loglik(css, n);
+}
+
+template <int K>
+__device__ double bq_css_ll_k(const double *__restrict__ row, int n, int p, int q, int I, const double *x) {
+#define BQ_CSS_CASE(P, Q, II)                                                                                         \
+    case (P) * 12 + (Q) * 2 + (II):                                                                                   \
+        if constexpr ((P) + (Q) + (II) == K) return bq_css_ll_t<P, Q, II>(row, n, x);                                 \
+        break;
+#define BQ_CSS_Q(P, Q) BQ_CSS_CASE(P, Q, 0) BQ_CSS_CASE(P, Q, 1)
+#define BQ_CSS_P(P) BQ_CSS_Q(P, 0) BQ_CSS_Q(P, 1) BQ_CSS_Q(P, 2) BQ_CSS_Q(P, 3) BQ_CSS_Q(P, 4) BQ_CSS_Q(P, 5)
+    switch (p * 12 + q * 2 + I) {
+        BQ_CSS_P(0) BQ_CSS_P(1) BQ_CSS_P(2) BQ_CSS_P(3) BQ_CSS_P(4) BQ_CSS_P(5)
+    default:
+        break;
+    }
+#undef BQ_CSS_P
+#undef BQ_CSS_Q
+#undef BQ_CSS_CASE
+    return bq_css_ll(row, n, p, q, I, x);          // unreachable for p, q <= 5 (the launchers' bounds)
+}
+
 struct BqObj {
     const double *y;
     int n, p, q, I;
@@ -82,9 +113,10 @@ struct BqObj {
 };
 
 // BaseOptimizer.computeObjectiveValue: counts, throws (TooManyEvaluations) past MaxEval; f = -LL (MAXIMIZE)
+template <int K>
 __device__ __forceinline__ int bq_eval(BqObj *o, const double *x, double *f) {
     if (++o->n_eval > o->max_eval) return 0;
-    *f = -bq_css_ll(o->y, o->n, o->p, o->q, o->I, x);
+    *f = -bq_css_ll_k<K>(o->y, o->n, o->p, o->q, o->I, x);
     return 1;
 }
 
@@ -105,10 +137,12 @@ __device__ __forceinline__ double bq_jmin(double a, double b) {
 }
 
 /* ---- TRSBOX (trust-region step of the quadratic model, bound tests inactive) ---------------------------- */
-__device__ void bq_trsbox(int n, int npt, const double *xpt, const double *xopt, const double *gopt, const double *hq,
+template <int NN>
+__device__ void bq_trsbox(const double *xpt, const double *xopt, const double *gopt, const double *hq,
                       const double *pq, const double *sl, const double *su, double delta, double *xnew, double *d,
                       double *gnew, double *xbdi, double *s, double *hs, double *hred, double *dsq_out,
                       double *crvmin_out) {
+    constexpr int n = NN, npt = 2 * NN + 1;
     int iterc = 0, nact = 0, itermax = 0, itcsav = 0, iact = 0, isav = 0, iu = 0;
     double beta = 0, stepsq = 0, gredsq = 0, delsq, qred, crvmin, resid, ds, shs, temp, blen, stplen, sdec, ggsav = 0;
     double dredsq = 0, dredg = 0, sredg = 0, angbd = 0, xsav = 0, dhs = 0, dhd = 0, redmax, redsav, rdprev = 0,
@@ -373,9 +407,11 @@ __device__ void bq_trsbox(int n, int npt, const double *xpt, const double *xopt,
 }
 
 /* ---- ALTMOV (alternative positions of the KNEW-th point, bound tests inactive) --------------------------- */
-__device__ void bq_altmov(int n, int npt, const double *xpt, const double *xopt, const double *bmat, const double *zmat,
+template <int NN>
+__device__ void bq_altmov(const double *xpt, const double *xopt, const double *bmat, const double *zmat,
                       const double *sl, const double *su, int kopt, int knew, double adelt, double *xnew,
                       double *xalt, double *alpha_out, double *cauchy_out, double *glag, double *hcol, double *w) {
+    constexpr int n = NN, npt = 2 * NN + 1;
     const int nptm = npt - n - 1;
     const double cnst = 1.0 + sqrt(2.0);
     double temp, alpha, ha, presav, step = 0, vlag, stpsav = 0, cauchy = 0, csave = 0, ggfree, wfixsq, wsqsav, gw,
@@ -540,8 +576,10 @@ __device__ void bq_altmov(int n, int npt, const double *xpt, const double *xopt,
 }
 
 /* ---- UPDATE (BMAT and ZMAT after moving the KNEW-th interpolation point) ---------------------------------- */
-__device__ void bq_update(int n, int npt, double *bmat, double *zmat, double *vlag, double beta, double denom, int knew,
+template <int NN>
+__device__ void bq_update(double *bmat, double *zmat, double *vlag, double beta, double denom, int knew,
                       double *w) {
+    constexpr int n = NN, npt = 2 * NN + 1;
     const int nptm = npt - n - 1;
     double ztest = 0.0, temp, tempa, tempb, alpha, tau;
     for (int k = 0; k < npt; k++)
@@ -582,11 +620,12 @@ __device__ void bq_update(int n, int npt, double *bmat, double *zmat, double *vl
 
 /* ---- BOBYQA driver + PRELIM + BOBYQB, unbounded, npt = 2n + 1 ------------------------------------------- *
  * Returns ARIMA_ST_*; x (in: the initial point, out: the optimum), n_eval_out = objective evaluations. */
+template <int NN>
 __device__ int bq_fit(const double *y, int len, int p, int q, int I, const double *x0, double *x_out, int *n_eval_out) {
-    const int n = I + p + q;
+    constexpr int n = NN;                                      /* = I + p + q (the launcher's instantiation) */
     *n_eval_out = 0;
     if (n < 2) return ARIMA_ST_TOO_FEW_PARAMS;                 /* BOBYQAOptimizer.setup: dimension >= 2 */
-    const int npt = 2 * n + 1, np = n + 1, nptm = npt - np, nh = (n * np) / 2, ndim = npt + n;
+    constexpr int npt = 2 * n + 1, np = n + 1, nptm = npt - np, nh = (n * np) / 2, ndim = npt + n;
     /* math.min(0.96, 0.2 * initParams.map(math.abs).max) (:147): Scala's max is reduceLeft((x, y) => if (x >= y) x
      * else y) with IEEE comparisons, Java's Math.min(a, b) is (a <= b ? a : b) for a = 0.96 -- NaN propagates as there */
     double amax = fabs(x0[0]);
@@ -633,7 +672,7 @@ __device__ int bq_fit(const double *y, int len, int p, int q, int I, const doubl
             XPT(nf - 1, nfx - 1) = stepb;
         }
         for (int j = 0; j < n; j++) x[j] = xbase[j] + XPT(nf - 1, j);   /* min(max(XL, .), XU): unbounded */
-        if (!bq_eval(&ob, x, &f)) { *n_eval_out = ob.n_eval - 1; return ARIMA_ST_MAX_EVAL; }
+        if (!bq_eval<NN>(&ob, x, &f)) { *n_eval_out = ob.n_eval - 1; return ARIMA_ST_MAX_EVAL; }
         fval[nf - 1] = f;
         if (nf == 1) {
             fbeg = f;
@@ -686,7 +725,12 @@ __device__ int bq_fit(const double *y, int len, int p, int q, int I, const doubl
            adelt = 0.0, alpha = 0.0, cauchy = 0.0, beta = 0.0, denom = 0.0, vquad = 0.0, diff = 0.0, fopt, densav;
     int state = 20;
     int status = ARIMA_ST_OK;
+    // Every evaluation of BOBYQB happens at ONE point of the loop, after the lane's state machine has run to its next
+    // evaluation request (state 360) or to its end: the lanes of a wave take different trust-region paths, and with the
+    // evaluation inside the switch a wave paid one full CSS pass per lane per request (the lanes' requests fall on
+    // different trips). Now the lanes reconverge before the pass and share it. Operation order per lane unchanged.
     for (;;) {
+      while (state >= 0 && state != 360) {
         switch (state) {
         case 20:
             if (kopt != kbase) {
@@ -708,7 +752,7 @@ __device__ int bq_fit(const double *y, int len, int p, int q, int I, const doubl
             }
             /* fallthrough */
         case 60:
-            bq_trsbox(n, npt, xpt, xopt, gopt, hq, pq, sl, su, delta, xnew, d, tw, tw + n, tw + 2 * n, tw + 3 * n,
+            bq_trsbox<NN>(xpt, xopt, gopt, hq, pq, sl, su, delta, xnew, d, tw, tw + n, tw + 2 * n, tw + 3 * n,
                       tw + 4 * n, &dsq, &crvmin);
             dnorm = bq_jmin(delta, sqrt(dsq));
             if (dnorm < 0.5 * rho) {
@@ -803,7 +847,7 @@ __device__ int bq_fit(const double *y, int len, int p, int q, int I, const doubl
             state = -1;
             break;
         case 210:
-            bq_altmov(n, npt, xpt, xopt, bmat, zmat, sl, su, kopt, knew, adelt, xnew, xalt, &alpha, &cauchy, tw,
+            bq_altmov<NN>(xpt, xopt, bmat, zmat, sl, su, kopt, knew, adelt, xnew, xalt, &alpha, &cauchy, tw,
                       tw + n, w);
             for (int i = 0; i < n; i++) d[i] = xnew[i] - xopt[i];
             /* fallthrough */
@@ -887,9 +931,7 @@ __device__ int bq_fit(const double *y, int len, int p, int q, int I, const doubl
             state = 360;
             break;
         }
-        case 360:
-            for (int i = 0; i < n; i++) x[i] = xbase[i] + xnew[i];     /* min(max(XL, .), XU): unbounded */
-            if (!bq_eval(&ob, x, &f)) { status = ARIMA_ST_MAX_EVAL; state = -1; break; }
+        case 361:                                                  /* after the evaluation at label 360 */
             nf++;
             if (ntrits == -1) {
                 fsave = f;
@@ -949,7 +991,7 @@ __device__ int bq_fit(const double *y, int len, int p, int q, int I, const doubl
                     }
                 }
             }
-            bq_update(n, npt, bmat, zmat, vlag, beta, denom, knew, w);
+            bq_update<NN>(bmat, zmat, vlag, beta, denom, knew, w);
             {
                 int ih = 0;
                 const double pqold = pq[knew];
@@ -1100,7 +1142,16 @@ __device__ int bq_fit(const double *y, int len, int p, int q, int I, const doubl
         default:
             break;
         }
-        if (state < 0) break;
+      }
+      if (state < 0) break;
+      /* label 360: the evaluation, the wave's lanes together */
+      for (int i = 0; i < n; i++) x[i] = xbase[i] + xnew[i];       /* min(max(XL, .), XU): unbounded */
+      if (!bq_eval<NN>(&ob, x, &f)) {
+          status = ARIMA_ST_MAX_EVAL;
+          state = -1;
+          break;
+      }
+      state = 361;
     }
     *n_eval_out = ob.n_eval > ob.max_eval ? ob.max_eval : ob.n_eval;
     if (state == -1) return status;
@@ -1144,6 +1195,7 @@ __device__ uint8_t bq_model_flags(const double *c, int p, int q, int I) {
 // One lane per series: fitModel's css-bobyqa branch after the initial parameters (ARIMA.scala:99-109): the
 // Hannan-Rissanen init (or the user's) from init / init_status. refit_status (optional, ARIMA.autoFit's
 // fitTryBothStrategies, :315-319): only the series whose css-cgd fit threw in the optimizer are refitted, in place.
+template <int NN>
 __global__ __launch_bounds__(64) void k_bobyqa_fit(const double *__restrict__ y, int64_t ld, int n, int64_t N, int p,
                                                    int q, int I, const double *__restrict__ init,
                                                    const int32_t *__restrict__ init_status,
@@ -1164,7 +1216,7 @@ __global__ __launch_bounds__(64) void k_bobyqa_fit(const double *__restrict__ y,
     double x0[BQ_KMAX], x[BQ_KMAX];
     int nev = 0;
     for (int j = 0; j < BQ_KMAX; ++j) x0[j] = j < k ? init[sid * k + j] : 0.0;
-    if (st == ARIMA_ST_OK) st = bq_fit(y + sid * ld, n, p, q, I, x0, x, &nev);
+    if (st == ARIMA_ST_OK) st = bq_fit<NN>(y + sid * ld, n, p, q, I, x0, x, &nev);
     const bool ok = st == ARIMA_ST_OK;
     for (int j = 0; j < k; ++j) coef_out[sid * k + j] = ok ? x[j] : __builtin_nan("");
     ll_out[sid] = ok ? bq_css_ll(y + sid * ld, n, p, q, I, x) : __builtin_nan("");
@@ -1174,14 +1226,116 @@ __global__ __launch_bounds__(64) void k_bobyqa_fit(const double *__restrict__ y,
     if (flags_out) flags_out[sid] = ok ? bq_model_flags(x, p, q, I) : (uint8_t)0;
 }
 
+// ---- autoFit's css-bobyqa retries of one round of the stepwise walk, in one launch ------------------------------
+// The round's candidate orders are fitted with css-cgd as separate batches (rows of order cb at [off[cb], off[cb+1])
+// of the round's result arrays, coefficients and inits k-strided from off[cb] * 11). A per-order css-bobyqa launch
+// would make each order wait for its slowest lane; instead the failing rows of every order are listed and refitted
+// together. Per row the same computation as k_bobyqa_fit with refit_status.
+__device__ __forceinline__ bool bq_refit_wanted(int rs) {
+    return rs == ARIMA_ST_MAX_EVAL || rs == ARIMA_ST_BRACKET_MAX_EVAL || rs == ARIMA_ST_MAX_ITER ||
+           rs == ARIMA_ST_BAD_INTERVAL;
+}
+
+__device__ __forceinline__ int af_row_combo(const int64_t *off, int64_t r) {   // the last order whose rows start <= r
+    int cb = 0;
+    for (int c = 1; c < kAfCombos; ++c)
+        if (off[c] <= r) cb = c;
+    return cb;
+}
+
+__global__ __launch_bounds__(64) void k_af_refit_list(const int32_t *__restrict__ status, int64_t total,
+                                                      const int64_t *__restrict__ off, int32_t *__restrict__ list,
+                                                      unsigned *__restrict__ count) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool want = false;
+    if (r < total && bq_refit_wanted(status[r])) {
+        const int cb = af_row_combo(off, r);
+        const int p = (cb / 2) / 3, q = (cb / 2) % 3;
+        want = !(p > 0 && q == 0);                 // the AR-only shortcut never reaches a method (ARIMA.scala:90-96)
+    }
+    const unsigned long long m = __ballot(want);
+    if (m == 0) return;
+    const int lane = threadIdx.x & 63;
+    unsigned base = 0;
+    if (lane == __ffsll((long long)m) - 1) base = atomicAdd(count, (unsigned)__popcll(m));
+    base = __shfl(base, __ffsll((long long)m) - 1);
+    if (want) list[base + __popcll(m & ((1ull << lane) - 1))] = (int32_t)r;
+}
+
+__global__ __launch_bounds__(64) void k_bobyqa_refit_rows(const double *__restrict__ rows, int64_t ld, int n,
+                                                          const int32_t *__restrict__ lists, int64_t N,
+                                                          const int64_t *__restrict__ off,
+                                                          const int32_t *__restrict__ list,
+                                                          const unsigned *__restrict__ count,
+                                                          const double *__restrict__ init,
+                                                          const int32_t *__restrict__ init_status,
+                                                          double *__restrict__ coef, double *__restrict__ ll,
+                                                          int32_t *__restrict__ status, uint8_t *__restrict__ flags) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)*count) return;
+    const int64_t r = list[i];
+    const int cb = af_row_combo(off, r);
+    const int p = (cb / 2) / 3, q = (cb / 2) % 3, I = cb % 2, k = I + p + q;
+    const int64_t slot = r - off[cb];
+    const double *y = rows + (int64_t)lists[(int64_t)cb * N + slot] * ld;
+    const int64_t base = off[cb] * 11 + slot * k;
+    int st = init_status[r];
+    double x0[BQ_KMAX], x[BQ_KMAX];
+    int nev = 0;
+    for (int j = 0; j < BQ_KMAX; ++j) x0[j] = j < k ? init[base + j] : 0.0;
+    if (st == ARIMA_ST_OK) {
+        switch (k) {                               // autoFit's orders: p <= 5, q <= 2
+        case 2: st = bq_fit<2>(y, n, p, q, I, x0, x, &nev); break;
+        case 3: st = bq_fit<3>(y, n, p, q, I, x0, x, &nev); break;
+        case 4: st = bq_fit<4>(y, n, p, q, I, x0, x, &nev); break;
+        case 5: st = bq_fit<5>(y, n, p, q, I, x0, x, &nev); break;
+        case 6: st = bq_fit<6>(y, n, p, q, I, x0, x, &nev); break;
+        case 7: st = bq_fit<7>(y, n, p, q, I, x0, x, &nev); break;
+        case 8: st = bq_fit<8>(y, n, p, q, I, x0, x, &nev); break;
+        default: st = ARIMA_ST_TOO_FEW_PARAMS; break;   /* k < 2: BOBYQAOptimizer.setup */
+        }
+    }
+    const bool ok = st == ARIMA_ST_OK;
+    for (int j = 0; j < k; ++j) coef[base + j] = ok ? x[j] : __builtin_nan("");
+    ll[r] = ok ? bq_css_ll(y, n, p, q, I, x) : __builtin_nan("");
+    status[r] = st;
+    flags[r] = ok ? bq_model_flags(x, p, q, I) : (uint8_t)0;
+}
+
+int launch_bobyqa_refit_round(const double *rows, int64_t ld, int n, const int32_t *lists, int64_t N,
+                              const int64_t *off, int64_t total, const double *init, const int32_t *init_status,
+                              int32_t *list, unsigned *count, double *coef, double *ll, int32_t *status,
+                              uint8_t *flags, hipStream_t s) {
+    if (total == 0) return ARIMA_OK;
+    if (hipMemsetAsync(count, 0, sizeof(unsigned), s) != hipSuccess) return ARIMA_E_DEVICE;
+    const dim3 grid((unsigned)((total + 63) / 64));
+    hipLaunchKernelGGL(k_af_refit_list, grid, dim3(64), 0, s, status, total, off, list, count);
+    hipLaunchKernelGGL(k_bobyqa_refit_rows, grid, dim3(64), 0, s, rows, ld, n, lists, N, off, list, count, init,
+                       init_status, coef, ll, status, flags);
+    return hipGetLastError() == hipSuccess ? ARIMA_OK : ARIMA_E_DEVICE;
+}
+
 int launch_bobyqa_fit(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, const double *init,
                       const int32_t *init_status, const int32_t *refit_status, double *coef_out, double *ll_out,
                       int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
                       hipStream_t s) {
     if (N == 0) return ARIMA_OK;
     if (p > 5 || q > 5 || I + p + q > BQ_KMAX) return ARIMA_E_UNSUPPORTED;
-    hipLaunchKernelGGL(k_bobyqa_fit, dim3((unsigned)((N + 63) / 64)), dim3(64), 0, s, y, ld, n, N, p, q, I, init,
-                       init_status, refit_status, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out);
+    // one instantiation per dimension k = I + p + q: Powell's loops get compile-time bounds, so they unroll and the
+    // short vectors (d, xopt, gopt, ...) live in registers instead of the lane's scratch
+    const dim3 grid((unsigned)((N + 63) / 64));
+#define BQ_LAUNCH(K)                                                                                                  \
+    case K:                                                                                                           \
+        hipLaunchKernelGGL(k_bobyqa_fit<K>, grid, dim3(64), 0, s, y, ld, n, N, p, q, I, init, init_status,            \
+                           refit_status, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out);            \
+        break;
+    switch (I + p + q) {
+        BQ_LAUNCH(0) BQ_LAUNCH(1) BQ_LAUNCH(2) BQ_LAUNCH(3) BQ_LAUNCH(4) BQ_LAUNCH(5) BQ_LAUNCH(6) BQ_LAUNCH(7)
+        BQ_LAUNCH(8) BQ_LAUNCH(9) BQ_LAUNCH(10) BQ_LAUNCH(11)
+    default:
+        return ARIMA_E_UNSUPPORTED;
+    }
+#undef BQ_LAUNCH
     return hipGetLastError() == hipSuccess ? ARIMA_OK : ARIMA_E_DEVICE;
 }
 

@@ -95,6 +95,14 @@ int launch_bobyqa_fit(const double *y, int64_t ld, int n, int64_t N, int p, int 
                       int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
                       hipStream_t s);
 
+// autoFit: the css-bobyqa retries of a whole round (every order's rows whose css-cgd fit threw in the optimizer), one
+// launch; rows = the differenced series (ld), lists / off = the round's per-order lists and row offsets, init /
+// init_status = each row's Hannan-Rissanen init (k-strided from off[cb] * 11) and status; list / count: workspace
+int launch_bobyqa_refit_round(const double *rows, int64_t ld, int n, const int32_t *lists, int64_t N,
+                              const int64_t *off, int64_t total, const double *init, const int32_t *init_status,
+                              int32_t *list, unsigned *count, double *coef, double *ll, int32_t *status,
+                              uint8_t *flags, hipStream_t s);
+
 int hr_shape_status_host(int n, int p, int q, int I);
 int ar_shape_status_host(int n, int p, int I);
 

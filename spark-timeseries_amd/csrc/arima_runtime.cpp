@@ -98,11 +98,25 @@ constexpr int kMaxPipeline = 8;
 // timing events, pinned counter copy, host-path staging). Fit calls rotate over h->pipeline contexts, so with
 // pipeline > 1 consecutive fits run concurrently and the tail of one fit kernel (its slowest series) overlaps the
 // next fit's differencing, init and bulk work; a context is reused only after its previous call has finished.
+// One device-fit call's caller buffers as byte ranges [lo, hi) (series rows and user inits read; the six outputs
+// written) -- fit_pipeline > 1 hazard tracking
+struct CallSpans {
+    uintptr_t in[2][2] = {}, out[6][2] = {};
+};
+constexpr int kInflightMax = 16;   // tracked calls per context; beyond, every later call waits for that context
+struct Inflight {                  // the device-fit calls on one context that may not have finished yet
+    CallSpans call[kInflightMax];
+    hipEvent_t ev[kInflightMax] = {};   // each call's end (a hazard waits for exactly that call)
+    int n = 0;
+    bool overflow = false;
+};
+
 struct FitCtx {
     hipStream_t stream = nullptr;
     hipEvent_t ev[kNumEvents] = {};
     hipEvent_t ev_done = nullptr;             // end of this context's last call
     bool has_done = false;
+    Inflight inflight;                        // its device-fit calls' caller buffers (fit_pipeline > 1)
     DevBuf diff;
     FitWs ws;
     unsigned long long *ctl_host = nullptr;   // pinned
@@ -114,6 +128,15 @@ struct FitCtx {
     size_t pin_bytes = 0;
     int64_t chunk_first = -1, chunk_n = 0;    // the chunk whose results wait in `pin`
 };
+
+inline void set_span(uintptr_t (&sp)[2], const void *p, int64_t bytes) {
+    sp[0] = (uintptr_t)p;
+    sp[1] = p && bytes > 0 ? (uintptr_t)p + (uintptr_t)bytes : (uintptr_t)p;
+}
+
+inline bool spans_meet(const uintptr_t (&a)[2], const uintptr_t (&b)[2]) {
+    return a[0] < a[1] && b[0] < b[1] && a[0] < b[1] && b[0] < a[1];
+}
 
 }  // namespace
 
@@ -146,7 +169,12 @@ struct arima_handle {
     int64_t last_express = 0;
     int64_t last_grid = 0;
     int search_lanes = 8;          // concurrent fits of the order search (2/4/8: 1269/1303/1408 series/s, profiles/r02/g_c5)
-    int pipeline = 1;              // fit contexts in rotation (option "fit_pipeline")
+    // fit contexts in rotation for device fits (option "fit_pipeline"). Default 3: consecutive asynchronous calls
+    // overlap (one call's tail with the next one's differencing, init and bulk passes) and calls that share buffers
+    // stay ordered (order_after_overlapping_fits). On the box's 4 hardware queues at C2 1M x 1024, 5 consecutive
+    // calls: 1 / 2 / 3 / 4 contexts 6.68 / 8.30 / 10.02 / 9.97 M series/s; one call alone 151 ms at 1, 162 ms at 3
+    // (drained bulk waves leave instead of turning express) -- profiles/r05/k_defp
+    int pipeline = 3;
     // one device fit call cut into this many slices on as many fit contexts (option "call_slices"; 1 = off, the
     // default; -1 = auto: 3 for a call of >= 3 x call_slice_min series at fit_pipeline 1 on the handle's own streams).
     // The slices of ONE call overlap while calls stay ordered (the next call waits for every slice). Measured on the
@@ -179,6 +207,7 @@ struct arima_handle {
     unsigned long long *search_acc_host = nullptr;   // pinned: (kCtlWords + 1) words per lane of the last search
     // autoFit (arima_autofit_batch*): the differenced rows, the walk state, the rounds' per-order lists and results
     DevBuf af_rows, af_dsel, af_state, af_best, af_counts, af_lists, af_off, af_coef, af_ll, af_status, af_flags;
+    DevBuf af_init, af_hrst, af_rlist, af_rcount;     // the round's inits and the css-bobyqa retry list
     DevBuf af_out_order, af_out_coef, af_out_aic, af_out_status, af_out_nfits;   // host-API staging
     int64_t *af_host = nullptr;                      // pinned: kAfCombos counts, then kAfCombos row offsets
     hipEvent_t ev_af = nullptr;
@@ -367,6 +396,8 @@ int arima_destroy(arima_handle *h) {
         for (auto &e : c.ev)
             if (e) hipEventDestroy(e);
         if (c.ev_done) hipEventDestroy(c.ev_done);
+        for (auto &e : c.inflight.ev)
+            if (e) hipEventDestroy(e);
         if (c.ctl_host) hipHostFree(c.ctl_host);
         if (c.pin) hipHostFree(c.pin);
     }
@@ -588,6 +619,69 @@ static hipError_t end_call(arima_handle *h, hipStream_t s) {
 static void begin_fit(arima_handle *h, FitCtx &c, hipStream_t s) {
     if (h->has_done) hipStreamWaitEvent(s, h->ev_done, 0);
     if (c.has_done) hipStreamWaitEvent(s, c.ev_done, 0);
+}
+
+// fit_pipeline > 1: consecutive fit calls run concurrently on different contexts, unless one reads what an in-flight
+// call writes, writes what it reads, or writes the same memory -- then the new call waits for that call's end (so a
+// caller may chain fits, e.g. one fit's coefficients as the next one's user inits, or reuse one output buffer,
+// without synchronising: the same results as fit_pipeline 1)
+static bool calls_meet(const CallSpans &x, const CallSpans &y) {
+    for (int a = 0; a < 6; ++a) {
+        for (int b = 0; b < 2; ++b)
+            if (spans_meet(x.out[a], y.in[b])) return true;
+        for (int b = 0; b < 6; ++b)
+            if (spans_meet(x.out[a], y.out[b])) return true;
+    }
+    for (int a = 0; a < 2; ++a)
+        for (int b = 0; b < 6; ++b)
+            if (spans_meet(x.in[a], y.out[b])) return true;
+    return false;
+}
+
+// Returns the event to record at the new call's end (nullptr once its context tracks kInflightMax calls).
+static hipEvent_t order_after_overlapping_fits(arima_handle *h, int ci, const CallSpans &cs, hipStream_t s) {
+    for (int j = 0; j < kMaxPipeline; ++j) {
+        FitCtx &o = h->fctx[j];
+        if (!o.has_done || hipEventQuery(o.ev_done) == hipSuccess) {   // everything issued there has finished
+            o.inflight.n = 0;
+            o.inflight.overflow = false;
+            continue;
+        }
+        if (j == ci) continue;                     // begin_fit already orders the call after its context's last one
+        if (o.inflight.overflow) {
+            hipStreamWaitEvent(s, o.ev_done, 0);
+            continue;
+        }
+        for (int e = 0; e < o.inflight.n; ++e)
+            if (calls_meet(cs, o.inflight.call[e])) hipStreamWaitEvent(s, o.inflight.ev[e], 0);
+    }
+    Inflight &f = h->fctx[ci].inflight;
+    if (f.n == kInflightMax) {
+        f.overflow = true;
+        return nullptr;
+    }
+    if (!f.ev[f.n] && hipEventCreateWithFlags(&f.ev[f.n], hipEventDisableTiming) != hipSuccess) {
+        f.overflow = true;
+        return nullptr;
+    }
+    f.call[f.n] = cs;
+    return f.ev[f.n++];
+}
+
+static CallSpans call_spans(const double *series, int64_t N, int32_t T, int64_t ld, int k, const double *uinit,
+                            const double *coef, const double *ll, const int32_t *st, const int32_t *ne,
+                            const int32_t *ng, const uint8_t *fl) {
+    CallSpans cs;
+    if (N <= 0) return cs;
+    set_span(cs.in[0], series, ((N - 1) * ld + std::max<int64_t>(T, 0)) * (int64_t)sizeof(double));
+    set_span(cs.in[1], uinit, N * k * (int64_t)sizeof(double));
+    set_span(cs.out[0], coef, N * k * (int64_t)sizeof(double));
+    set_span(cs.out[1], ll, N * (int64_t)sizeof(double));
+    set_span(cs.out[2], st, N * (int64_t)sizeof(int32_t));
+    set_span(cs.out[3], ne, N * (int64_t)sizeof(int32_t));
+    set_span(cs.out[4], ng, N * (int64_t)sizeof(int32_t));
+    set_span(cs.out[5], fl, N);
+    return cs;
 }
 
 static hipError_t end_fit(FitCtx &c, hipStream_t s) {
@@ -866,10 +960,17 @@ int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_se
         FitCtx &c = h->fctx[ci];
         hipStream_t s = stream ? (hipStream_t)stream : c.stream;
         begin_fit(h, c, s);
+        hipEvent_t ev_call = nullptr;
+        if (P > 1)
+            ev_call = order_after_overlapping_fits(h, ci, call_spans(d_series, n_series, T, ld,
+                                                                     include_intercept + p + q, d_user_init,
+                                                                     d_coef_out, d_css_ll_out, d_status_out,
+                                                                     d_n_eval_out, d_n_grad_out, d_flags_out), s);
         const int rc = fit_device_locked(h, c, ci, P, d_series, n_series, T, ld, p, d, q, include_intercept, method,
                                          d_user_init, d_coef_out, d_css_ll_out, d_status_out, d_n_eval_out,
                                          d_n_grad_out, d_flags_out, s, P > 1);
         HIPCHK(h, end_fit(c, s));
+        if (ev_call) HIPCHK(h, hipEventRecord(ev_call, s));
         return rc;
     }
     // sliced: slice j of the batch runs on the next fit context (its own outputs' rows), exactly as consecutive calls
@@ -909,12 +1010,20 @@ int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_se
         FitCtx &c = h->fctx[ci];
         hipStream_t s = stream ? (hipStream_t)stream : c.stream;
         begin_fit(h, c, s);
+        hipEvent_t ev_call = nullptr;
+        if (P > 1)
+            ev_call = order_after_overlapping_fits(
+                h, ci, call_spans(d_series + f * ld, ns, T, ld, k, d_user_init ? d_user_init + f * k : nullptr,
+                                  d_coef_out + f * k, d_css_ll_out + f, d_status_out + f,
+                                  d_n_eval_out ? d_n_eval_out + f : nullptr, d_n_grad_out ? d_n_grad_out + f : nullptr,
+                                  d_flags_out ? d_flags_out + f : nullptr), s);
         const int rc = fit_device_locked(
             h, c, ci, PC, d_series + f * ld, ns, T, ld, p, d, q, include_intercept, method,
             d_user_init ? d_user_init + f * k : nullptr, d_coef_out + f * k, d_css_ll_out + f, d_status_out + f,
             d_n_eval_out ? d_n_eval_out + f : nullptr, d_n_grad_out ? d_n_grad_out + f : nullptr,
             d_flags_out ? d_flags_out + f : nullptr, s, PC > 1, sl);
         HIPCHK(h, end_fit(c, s));
+        if (ev_call) HIPCHK(h, hipEventRecord(ev_call, s));
         h->slice_n++;
         if (rc != ARIMA_OK) return rc;
     }
@@ -1588,6 +1697,10 @@ static int autofit_locked(arima_handle *h, const double *d_series, int64_t N, in
     RCCHK(h, h->af_ll.ensure((size_t)rows_max * sizeof(double)), "autofit workspace");
     RCCHK(h, h->af_status.ensure((size_t)rows_max * sizeof(int32_t)), "autofit workspace");
     RCCHK(h, h->af_flags.ensure((size_t)rows_max), "autofit workspace");
+    RCCHK(h, h->af_init.ensure((size_t)rows_max * 11 * sizeof(double)), "autofit workspace");
+    RCCHK(h, h->af_hrst.ensure((size_t)rows_max * sizeof(int32_t)), "autofit workspace");
+    RCCHK(h, h->af_rlist.ensure((size_t)rows_max * sizeof(int32_t)), "autofit workspace");
+    RCCHK(h, h->af_rcount.ensure(sizeof(unsigned)), "autofit workspace");
     if (!h->af_host && hipHostMalloc((void **)&h->af_host, 2 * kAfCombos * sizeof(int64_t), 0) != hipSuccess)
         return set_err(h, ARIMA_E_OOM, "pinned");
     if (!h->ev_af) HIPCHK(h, hipEventCreateWithFlags(&h->ev_af, hipEventDisableTiming));
@@ -1654,18 +1767,27 @@ static int autofit_locked(arima_handle *h, const double *d_series, int64_t N, in
                                  h->af_coef.as<double>() + off[cb] * 11, h->af_ll.as<double>() + off[cb],
                                  h->af_status.as<int32_t>() + off[cb], nullptr, nullptr,
                                  h->af_flags.as<uint8_t>() + off[cb], c.stream, nullptr, &gridb, &xb, P > 1), "fit");
-            // fitTryBothStrategies (:315-319): the series whose css-cgd fit threw in the optimizer, refitted with
-            // css-bobyqa from the same Hannan-Rissanen init, in place (the AR-only shortcut never reaches a method)
+            // the Hannan-Rissanen inits and their status, kept for the round's css-bobyqa retries (below)
+            const int k = p + q + I;
+            if (!(p > 0 && q == 0) && k > 0) {
+                HIPCHK(h, hipMemcpyAsync(h->af_init.as<double>() + off[cb] * 11, c.ws.init.ptr,
+                                         (size_t)cnt * k * sizeof(double), hipMemcpyDeviceToDevice, c.stream));
+            }
             if (!(p > 0 && q == 0))
-                RCCHK(h, sts::launch_bobyqa_fit(c.diff.as<double>(), ldT, T, cnt, p, q, I, c.ws.init.as<double>(),
-                                                c.ws.hr_status.as<int32_t>(), h->af_status.as<int32_t>() + off[cb],
-                                                h->af_coef.as<double>() + off[cb] * 11, h->af_ll.as<double>() + off[cb],
-                                                h->af_status.as<int32_t>() + off[cb], nullptr, nullptr,
-                                                h->af_flags.as<uint8_t>() + off[cb], c.stream), "bobyqa refit");
+                HIPCHK(h, hipMemcpyAsync(h->af_hrst.as<int32_t>() + off[cb], c.ws.hr_status.ptr,
+                                         (size_t)cnt * sizeof(int32_t), hipMemcpyDeviceToDevice, c.stream));
             HIPCHK(h, end_fit(c, c.stream));
             ++used;
         }
         for (int j = 0; j < std::min(used, P); ++j) HIPCHK(h, hipStreamWaitEvent(s, h->fctx[j].ev_done, 0));
+        // fitTryBothStrategies (:315-319): every row of the round whose css-cgd fit threw in the optimizer, refitted
+        // with css-bobyqa from the same Hannan-Rissanen init, in place -- one launch for all the round's orders
+        RCCHK(h, sts::launch_bobyqa_refit_round(h->af_rows.as<double>(), ldT, T, h->af_lists.as<int32_t>(), N,
+                                                h->af_off.as<int64_t>(), total, h->af_init.as<double>(),
+                                                h->af_hrst.as<int32_t>(), h->af_rlist.as<int32_t>(),
+                                                h->af_rcount.as<unsigned>(), h->af_coef.as<double>(),
+                                                h->af_ll.as<double>(), h->af_status.as<int32_t>(),
+                                                h->af_flags.as<uint8_t>(), s), "bobyqa refit");
         RCCHK(h, sts::launch_af_update(N, st, h->af_off.as<int64_t>(), h->af_coef.as<double>(), h->af_ll.as<double>(),
                                        h->af_status.as<int32_t>(), h->af_flags.as<uint8_t>(), h->af_best.as<double>(),
                                        max_p, max_q, s), "autofit update");

@@ -464,6 +464,8 @@ def test_pipelined_device_fits_match_serial(engine, pipeline):
     s = _device_sample(engine, N, T, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 99)
     orders = [(2, 1, 2, 1), (1, 1, 1, 1), (2, 1, 2, 1), (3, 1, 2, 0), (2, 1, 2, 1)]
 
+    prev = engine.get_option("fit_pipeline")
+
     def run(P):
         engine.set_option("fit_pipeline", P)
         outs = []
@@ -479,13 +481,59 @@ def test_pipelined_device_fits_match_serial(engine, pipeline):
                 outs.append(r)
             engine.synchronize()
         finally:
-            engine.set_option("fit_pipeline", 1)
+            engine.set_option("fit_pipeline", prev)
         return [[t.cpu().numpy() for t in r] for r in outs]
 
     a, b = run(1), run(pipeline)
     for i, (ra, rb) in enumerate(zip(a, b)):
         for x, y in zip(ra, rb):
             assert _same(x, y), (pipeline, orders[i])
+
+
+def test_pipelined_fits_that_share_buffers_stay_ordered(engine):
+    # fit_pipeline > 1 (the default is 3): a call that reads an in-flight call's outputs (read after write), writes
+    # what one reads (write after read) or writes the same outputs (write after write) waits for it, so chained and
+    # buffer-reusing asynchronous calls give the serial (fit_pipeline 1) results bit for bit
+    import torch
+    N, T = 1 << 15, 1024
+    s1 = _device_sample(engine, N, T, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 71)
+    s2 = _device_sample(engine, N, T, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 72)
+    dev = s1.device
+
+    def outs(k=5):
+        return [torch.empty((N, k), dtype=torch.float64, device=dev), torch.empty(N, dtype=torch.float64, device=dev)] + \
+            [torch.empty(N, dtype=torch.int32, device=dev) for _ in range(3)] + \
+            [torch.empty(N, dtype=torch.uint8, device=dev)]
+
+    def fit(series, o, init=None):
+        engine.fit_batch_device(series.data_ptr(), N, T, T, 2, 1, 2, 1, *[t.data_ptr() for t in o],
+                                d_user_init=None if init is None else init.data_ptr(), blocking=False)
+
+    def scenario():
+        a, b, c = outs(), outs(), outs()
+        z = s2.clone()
+        fit(s1, a)
+        fit(s2, b, init=a[0])          # RAW: b starts from a's coefficients
+        fit(z, c)                      # c reads z ...
+        zl = outs()
+        zl[1] = z[:, 0]                # ... while the next call writes its ll into z's first column: WAR
+        fit(s1, zl)
+        fit(s1, b)                     # WAW: b's buffers rewritten by a fit of s1
+        engine.synchronize()
+        return [[t.cpu().numpy() for t in r] for r in (a, b, c)]
+
+    prev = engine.get_option("fit_pipeline")
+    try:
+        engine.set_option("fit_pipeline", 1)
+        serial = scenario()
+        engine.set_option("fit_pipeline", 3)
+        piped = scenario()
+    finally:
+        engine.set_option("fit_pipeline", prev)
+    for ra, rb in zip(serial, piped):
+        for x, y in zip(ra, rb):
+            assert _same(x, y)
+    assert _same(piped[1][0], piped[0][0])      # the WAW's final contents: s1's fit, as the first call's
 
 
 @pytest.mark.parametrize("xblocks", [-1, 0])
@@ -555,6 +603,8 @@ def test_express_ring_under_pressure_matches_bulk(engine):
     N, T = 1 << 16, 1024
     s = _device_sample(engine, N, T, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 20261015)
     outs = {}
+    prev = engine.get_option("fit_pipeline")
+    engine.set_option("fit_pipeline", 1)      # drained bulk waves turn express only when no other fit may follow
     for xb in (0, -1):
         engine.set_option("express_blocks", xb)
         try:
@@ -567,6 +617,7 @@ def test_express_ring_under_pressure_matches_bulk(engine):
         finally:
             engine.set_option("express_blocks", -1)
         outs[xb] = ([t.cpu().numpy() for t in r], st)
+    engine.set_option("fit_pipeline", prev)
     (a, _), (b, st) = outs[0], outs[-1]
     assert st["express_series"] > 1000, st
     for x, y in zip(a, b):
@@ -679,6 +730,7 @@ def test_sliced_device_fit_matches_unsliced(engine, pipeline, N):
         engine.fit_batch_device(s.data_ptr(), N, T, T, 2, 1, 2, True, *[t.data_ptr() for t in r])
         return [t.cpu().numpy() for t in r], engine.stats()
 
+    prev = engine.get_option("fit_pipeline")
     whole, st_whole = run()
     engine.set_option("fit_slice_bytes", 1024 * 1024 * 8)
     engine.set_option("fit_pipeline", pipeline)
@@ -686,7 +738,7 @@ def test_sliced_device_fit_matches_unsliced(engine, pipeline, N):
         sliced, st = run()
     finally:
         engine.set_option("fit_slice_bytes", 0)
-        engine.set_option("fit_pipeline", 1)
+        engine.set_option("fit_pipeline", prev)
     for x, y in zip(whole, sliced):
         assert _same(x, y)
     assert st["n_series"] == N and st["n_eval"] == int(whole[3].sum()) and st["n_grad"] == int(whole[4].sum()), st

@@ -1,5 +1,6 @@
 """Probe: the cost of the css-bobyqa device fit (k_bobyqa_fit) and of autoFit at growing batch sizes on the C2
-series generator. Prints one JSON line per measurement (run on the GPU box: python tools/bobyqa_probe.py [N ...])."""
+series generator. Prints one JSON line per measurement (run on the GPU box: python tools/bobyqa_probe.py [N ...]).
+PROBE_WHAT=bobyqa runs only the css-bobyqa fits (for counter passes)."""
 import json
 import os
 import sys
@@ -26,7 +27,10 @@ def main():
         ll = torch.empty(N, dtype=torch.float64, device="cuda")
         st = torch.empty(N, dtype=torch.int32, device="cuda")
         ne = torch.empty(N, dtype=torch.int32, device="cuda")
+        only = os.environ.get("PROBE_WHAT", "")
         for method, name in ((L.METHOD_CSS_CGD, "css-cgd"), (1, "css-bobyqa")):
+            if only and only not in name:
+                continue
             t0 = time.perf_counter()
             eng.fit_batch_device(s.data_ptr(), N, T, T, 2, 1, 2, True, coef.data_ptr(), ll.data_ptr(), st.data_ptr(),
                                  d_n_eval=ne.data_ptr(), method=method)
@@ -37,6 +41,8 @@ def main():
                               "n_eval_max": int(n_eval.max()),
                               "status": {str(k): int(v) for k, v in zip(*np.unique(st.cpu().numpy(),
                                                                                   return_counts=True))}}), flush=True)
+        if only:
+            continue
         t0 = time.perf_counter()
         r = eng.autofit(s.cpu().numpy(), 5, 2, 5)
         dt = time.perf_counter() - t0
