@@ -5,22 +5,33 @@
 // logLikelihoodCSSARMA, MaxEval(10000). k_bobyqa_fit gives every series a lane that runs Powell's routines (PRELIM,
 // BOBYQB, TRSBOX, ALTMOV, UPDATE) for that configuration in their published operation order -- with infinite bounds
 // every bound test is inactive -- and evaluates the objective by streaming its own row (bq_css_ll: the CSS recursion
-// of ARIMA.scala:430-445 / 581-618 with runtime orders, the same operations as css_pass). The interpolation state
-// (~10 KB per series: XPT, BMAT, ZMAT, the quadratic model) lives in the lane's private (scratch) memory.
+// of ARIMA.scala:430-445 / 581-618, css_pass's operations). The interpolation state (XPT, BMAT, ZMAT, the quadratic
+// model: 2.9 KB at k = 5, 6 KB at k = 8) is a BqState<k>.
 // As in the oracle (oracle/bobyqa_oracle.c), Powell's RESCUE is not restated: a fit that reaches it reports
-// ARIMA_ST_BOBYQA_RESCUE. Lanes diverge (every series takes its own trust-region path): the kernel is a correct
-// fallback, not a tuned one; css-cgd stays the headline path.
+// ARIMA_ST_BOBYQA_RESCUE. Two layouts, bit-identical: a lane per series (the state in private memory; lanes diverge,
+// every series takes its own trust-region path) for large batches, and a wave per series (the state in LDS, the
+// wave's lanes run one series' uniform code: no divergence, LDS instead of scratch latency) for small batches and
+// autoFit's retries, whose time is set by their slowest series.
 #include "arima_device.hpp"
 #include "arima_launch.hpp"
 
 namespace sts {
 
 #define BQ_KMAX 11
-#define BQ_NPTMAX (2 * BQ_KMAX + 1)
-#define BQ_NDIMMAX (BQ_NPTMAX + BQ_KMAX)
-#define XPT(k, j) xpt[(k) * BQ_KMAX + (j)]
-#define BMAT(i, j) bmat[(i) * BQ_KMAX + (j)]
-#define ZMAT(k, j) zmat[(k) * BQ_KMAX + (j)]
+// row-major interpolation matrices with the dimension's own stride (every routine is templated on it, NN)
+#define BQ_S (NN > 0 ? NN : 1)
+#define XPT(k, j) xpt[(k) * BQ_S + (j)]
+#define BMAT(i, j) bmat[(i) * BQ_S + (j)]
+#define ZMAT(k, j) zmat[(k) * BQ_S + (j)]
+
+// One fit's BOBYQA state for dimension NN (npt = 2 NN + 1 interpolation points, ndim = npt + NN): in the lane's
+// private memory (k_bobyqa_fit: a lane per series) or in LDS (k_bobyqa_fit_wave: a wave per series).
+template <int NN>
+struct BqState {
+    static constexpr int N1 = NN > 0 ? NN : 1, NPT = 2 * N1 + 1, NDIM = NPT + N1;
+    double xbase[N1], xpt[NPT * N1], fval[NPT], xopt[N1], gopt[N1], hq[N1 * (N1 + 1) / 2], pq[NPT], bmat[NDIM * N1],
+        zmat[NPT * N1], sl[N1], su[N1], xnew[N1], xalt[N1], d[N1], vlag[NDIM], w[3 * NDIM], x[N1], tw[5 * N1];
+};
 
 // logLikelihoodCSSARMA (ARIMA.scala:430-445, iterateARMA :581-618, updateMAErrors :544-554) at runtime orders
 // p, q <= 5: the operations of css_pass in the same order (dest = 0 + I * c0, + AR lags, + MA terms; the ascending
@@ -138,7 +149,7 @@ __device__ __forceinline__ double bq_jmin(double a, double b) {
 
 /* ---- TRSBOX (trust-region step of the quadratic model, bound tests inactive) ---------------------------- */
 template <int NN>
-__device__ void bq_trsbox(const double *xpt, const double *xopt, const double *gopt, const double *hq,
+__device__ __forceinline__ void bq_trsbox(const double *xpt, const double *xopt, const double *gopt, const double *hq,
                       const double *pq, const double *sl, const double *su, double delta, double *xnew, double *d,
                       double *gnew, double *xbdi, double *s, double *hs, double *hred, double *dsq_out,
                       double *crvmin_out) {
@@ -408,7 +419,7 @@ __device__ void bq_trsbox(const double *xpt, const double *xopt, const double *g
 
 /* ---- ALTMOV (alternative positions of the KNEW-th point, bound tests inactive) --------------------------- */
 template <int NN>
-__device__ void bq_altmov(const double *xpt, const double *xopt, const double *bmat, const double *zmat,
+__device__ __forceinline__ void bq_altmov(const double *xpt, const double *xopt, const double *bmat, const double *zmat,
                       const double *sl, const double *su, int kopt, int knew, double adelt, double *xnew,
                       double *xalt, double *alpha_out, double *cauchy_out, double *glag, double *hcol, double *w) {
     constexpr int n = NN, npt = 2 * NN + 1;
@@ -577,7 +588,7 @@ __device__ void bq_altmov(const double *xpt, const double *xopt, const double *b
 
 /* ---- UPDATE (BMAT and ZMAT after moving the KNEW-th interpolation point) ---------------------------------- */
 template <int NN>
-__device__ void bq_update(double *bmat, double *zmat, double *vlag, double beta, double denom, int knew,
+__device__ __forceinline__ void bq_update(double *bmat, double *zmat, double *vlag, double beta, double denom, int knew,
                       double *w) {
     constexpr int n = NN, npt = 2 * NN + 1;
     const int nptm = npt - n - 1;
@@ -621,7 +632,8 @@ __device__ void bq_update(double *bmat, double *zmat, double *vlag, double beta,
 /* ---- BOBYQA driver + PRELIM + BOBYQB, unbounded, npt = 2n + 1 ------------------------------------------- *
  * Returns ARIMA_ST_*; x (in: the initial point, out: the optimum), n_eval_out = objective evaluations. */
 template <int NN>
-__device__ int bq_fit(const double *y, int len, int p, int q, int I, const double *x0, double *x_out, int *n_eval_out) {
+__device__ __forceinline__ int bq_fit(const double *y, int len, int p, int q, int I, const double *x0, double *x_out,
+                                      int *n_eval_out, BqState<NN> &S) {
     constexpr int n = NN;                                      /* = I + p + q (the launcher's instantiation) */
     *n_eval_out = 0;
     if (n < 2) return ARIMA_ST_TOO_FEW_PARAMS;                 /* BOBYQAOptimizer.setup: dimension >= 2 */
@@ -634,13 +646,12 @@ __device__ int bq_fit(const double *y, int len, int p, int q, int I, const doubl
     const double rhobeg = (0.96 <= r02) ? 0.96 : r02;
     const double rhoend = rhobeg * 1e-6;                       /* :148 */
     BqObj ob{y, len, p, q, I, 0, 10000};
-    double xbase[BQ_KMAX], xpt[BQ_NPTMAX * BQ_KMAX], fval[BQ_NPTMAX], xopt[BQ_KMAX], gopt[BQ_KMAX],
-        hq[BQ_KMAX * (BQ_KMAX + 1) / 2], pq[BQ_NPTMAX], bmat[BQ_NDIMMAX * BQ_KMAX], zmat[BQ_NPTMAX * BQ_KMAX],
-        sl[BQ_KMAX], su[BQ_KMAX], xnew[BQ_KMAX], xalt[BQ_KMAX], d[BQ_KMAX], vlag[BQ_NDIMMAX],
-        w[3 * BQ_NDIMMAX], x[BQ_KMAX], tw[5 * BQ_KMAX];
-    for (int i = 0; i < BQ_NPTMAX * BQ_KMAX; i++) xpt[i] = 0.0;
-    for (int i = 0; i < BQ_NDIMMAX * BQ_KMAX; i++) bmat[i] = 0.0;
-    for (int i = 0; i < BQ_NPTMAX * BQ_KMAX; i++) zmat[i] = 0.0;
+    double *xbase = S.xbase, *xpt = S.xpt, *fval = S.fval, *xopt = S.xopt, *gopt = S.gopt, *hq = S.hq, *pq = S.pq,
+           *bmat = S.bmat, *zmat = S.zmat, *sl = S.sl, *su = S.su, *xnew = S.xnew, *xalt = S.xalt, *d = S.d,
+           *vlag = S.vlag, *w = S.w, *x = S.x, *tw = S.tw;
+    for (int i = 0; i < BqState<NN>::NPT * BqState<NN>::N1; i++) xpt[i] = 0.0;
+    for (int i = 0; i < BqState<NN>::NDIM * BqState<NN>::N1; i++) bmat[i] = 0.0;
+    for (int i = 0; i < BqState<NN>::NPT * BqState<NN>::N1; i++) zmat[i] = 0.0;
     for (int j = 0; j < n; j++) {                              /* BOBYQA: SL = XL - X, SU = XU - X (unbounded) */
         x[j] = x0[j];
         sl[j] = -__builtin_inf();
@@ -1192,38 +1203,55 @@ __device__ uint8_t bq_model_flags(const double *c, int p, int q, int I) {
     return (uint8_t)((st ? ARIMA_FLAG_STATIONARY : 0) | (inv ? ARIMA_FLAG_INVERTIBLE : 0));
 }
 
-// One lane per series: fitModel's css-bobyqa branch after the initial parameters (ARIMA.scala:99-109): the
-// Hannan-Rissanen init (or the user's) from init / init_status. refit_status (optional, ARIMA.autoFit's
-// fitTryBothStrategies, :315-319): only the series whose css-cgd fit threw in the optimizer are refitted, in place.
-template <int NN>
-__global__ __launch_bounds__(64) void k_bobyqa_fit(const double *__restrict__ y, int64_t ld, int n, int64_t N, int p,
+// fitModel's css-bobyqa branch after the initial parameters (ARIMA.scala:99-109): the Hannan-Rissanen init (or the
+// user's) from init / init_status. refit_status (optional, ARIMA.autoFit's fitTryBothStrategies, :315-319): only the
+// series whose css-cgd fit threw in the optimizer are refitted, in place.
+// WAVE = false: a lane per series, the state in the lane's private memory. WAVE = true: a wave per series, the state
+// in LDS; every lane runs the same (uniform) code on the same values, so the wave never diverges and every access
+// to the interpolation matrices is an LDS broadcast instead of a scratch round trip; lane 0 writes the outputs.
+// resident waves per SIMD the wave kernels are compiled for (a register cap): 1 (512 VGPRs) / 2 (256) / 4 (128, with
+// spills): css-bobyqa fits of 65 536 C2 series 5.86 / 3.56 / 7.00 s, autoFit of 65 536 12.25 / 11.98 / 13.4 s
+// (profiles/r05/q_wave, r_occ2, r_occ4)
+constexpr int kBqWaveOcc = 2;
+
+__device__ __forceinline__ bool bq_refit_wanted(int rs) {
+    return rs == ARIMA_ST_MAX_EVAL || rs == ARIMA_ST_BRACKET_MAX_EVAL || rs == ARIMA_ST_MAX_ITER ||
+           rs == ARIMA_ST_BAD_INTERVAL;
+}
+
+template <int NN, bool WAVE>
+__global__ __launch_bounds__(64, WAVE ? kBqWaveOcc : 1) void k_bobyqa_fit(const double *__restrict__ y, int64_t ld, int n, int64_t N, int p,
                                                    int q, int I, const double *__restrict__ init,
                                                    const int32_t *__restrict__ init_status,
                                                    const int32_t *__restrict__ refit_status,
                                                    double *__restrict__ coef_out, double *__restrict__ ll_out,
                                                    int32_t *__restrict__ status_out, int32_t *__restrict__ n_eval_out,
                                                    int32_t *__restrict__ n_grad_out, uint8_t *__restrict__ flags_out) {
-    const int64_t sid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t sid = WAVE ? (int64_t)blockIdx.x : (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (sid >= N) return;
-    if (refit_status) {
-        const int rs = refit_status[sid];
-        if (!(rs == ARIMA_ST_MAX_EVAL || rs == ARIMA_ST_BRACKET_MAX_EVAL || rs == ARIMA_ST_MAX_ITER ||
-              rs == ARIMA_ST_BAD_INTERVAL))
-            return;
-    }
+    if (refit_status && !bq_refit_wanted(refit_status[sid])) return;
     const int k = I + p + q;
     int st = init_status ? init_status[sid] : ARIMA_ST_OK;
     double x0[BQ_KMAX], x[BQ_KMAX];
     int nev = 0;
     for (int j = 0; j < BQ_KMAX; ++j) x0[j] = j < k ? init[sid * k + j] : 0.0;
-    if (st == ARIMA_ST_OK) st = bq_fit<NN>(y + sid * ld, n, p, q, I, x0, x, &nev);
+    if constexpr (WAVE) {
+        __shared__ BqState<NN> S;
+        if (st == ARIMA_ST_OK) st = bq_fit<NN>(y + sid * ld, n, p, q, I, x0, x, &nev, S);
+    } else {
+        BqState<NN> S;
+        if (st == ARIMA_ST_OK) st = bq_fit<NN>(y + sid * ld, n, p, q, I, x0, x, &nev, S);
+    }
     const bool ok = st == ARIMA_ST_OK;
+    const double ll = ok ? bq_css_ll(y + sid * ld, n, p, q, I, x) : __builtin_nan("");
+    const uint8_t fl = ok ? bq_model_flags(x, p, q, I) : (uint8_t)0;
+    if (WAVE && threadIdx.x != 0) return;
     for (int j = 0; j < k; ++j) coef_out[sid * k + j] = ok ? x[j] : __builtin_nan("");
-    ll_out[sid] = ok ? bq_css_ll(y + sid * ld, n, p, q, I, x) : __builtin_nan("");
+    ll_out[sid] = ll;
     status_out[sid] = st;
     if (n_eval_out) n_eval_out[sid] = nev;
     if (n_grad_out) n_grad_out[sid] = 0;
-    if (flags_out) flags_out[sid] = ok ? bq_model_flags(x, p, q, I) : (uint8_t)0;
+    if (flags_out) flags_out[sid] = fl;
 }
 
 // ---- autoFit's css-bobyqa retries of one round of the stepwise walk, in one launch ------------------------------
@@ -1231,11 +1259,6 @@ __global__ __launch_bounds__(64) void k_bobyqa_fit(const double *__restrict__ y,
 // of the round's result arrays, coefficients and inits k-strided from off[cb] * 11). A per-order css-bobyqa launch
 // would make each order wait for its slowest lane; instead the failing rows of every order are listed and refitted
 // together. Per row the same computation as k_bobyqa_fit with refit_status.
-__device__ __forceinline__ bool bq_refit_wanted(int rs) {
-    return rs == ARIMA_ST_MAX_EVAL || rs == ARIMA_ST_BRACKET_MAX_EVAL || rs == ARIMA_ST_MAX_ITER ||
-           rs == ARIMA_ST_BAD_INTERVAL;
-}
-
 __device__ __forceinline__ int af_row_combo(const int64_t *off, int64_t r) {   // the last order whose rows start <= r
     int cb = 0;
     for (int c = 1; c < kAfCombos; ++c)
@@ -1262,7 +1285,19 @@ __global__ __launch_bounds__(64) void k_af_refit_list(const int32_t *__restrict_
     if (want) list[base + __popcll(m & ((1ull << lane) - 1))] = (int32_t)r;
 }
 
-__global__ __launch_bounds__(64) void k_bobyqa_refit_rows(const double *__restrict__ rows, int64_t ld, int n,
+template <int K, bool WAVE>
+__device__ __forceinline__ int bq_fit_k(const double *y, int n, int p, int q, int I, const double *x0, double *x,
+                                        int *nev, double *smem) {
+    if constexpr (WAVE) {
+        return bq_fit<K>(y, n, p, q, I, x0, x, nev, *reinterpret_cast<BqState<K> *>(smem));
+    } else {
+        BqState<K> S;
+        return bq_fit<K>(y, n, p, q, I, x0, x, nev, S);
+    }
+}
+
+template <bool WAVE>
+__global__ __launch_bounds__(64, WAVE ? kBqWaveOcc : 1) void k_bobyqa_refit_rows(const double *__restrict__ rows, int64_t ld, int n,
                                                           const int32_t *__restrict__ lists, int64_t N,
                                                           const int64_t *__restrict__ off,
                                                           const int32_t *__restrict__ list,
@@ -1271,7 +1306,9 @@ __global__ __launch_bounds__(64) void k_bobyqa_refit_rows(const double *__restri
                                                           const int32_t *__restrict__ init_status,
                                                           double *__restrict__ coef, double *__restrict__ ll,
                                                           int32_t *__restrict__ status, uint8_t *__restrict__ flags) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    constexpr int kSmem = WAVE ? (int)(sizeof(BqState<8>) / sizeof(double)) : 1;
+    __shared__ double smem[kSmem];                 // the largest autoFit dimension: p <= 5, q <= 2, intercept
+    const int64_t i = WAVE ? (int64_t)blockIdx.x : (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (int64_t)*count) return;
     const int64_t r = list[i];
     const int cb = af_row_combo(off, r);
@@ -1285,49 +1322,61 @@ __global__ __launch_bounds__(64) void k_bobyqa_refit_rows(const double *__restri
     for (int j = 0; j < BQ_KMAX; ++j) x0[j] = j < k ? init[base + j] : 0.0;
     if (st == ARIMA_ST_OK) {
         switch (k) {                               // autoFit's orders: p <= 5, q <= 2
-        case 2: st = bq_fit<2>(y, n, p, q, I, x0, x, &nev); break;
-        case 3: st = bq_fit<3>(y, n, p, q, I, x0, x, &nev); break;
-        case 4: st = bq_fit<4>(y, n, p, q, I, x0, x, &nev); break;
-        case 5: st = bq_fit<5>(y, n, p, q, I, x0, x, &nev); break;
-        case 6: st = bq_fit<6>(y, n, p, q, I, x0, x, &nev); break;
-        case 7: st = bq_fit<7>(y, n, p, q, I, x0, x, &nev); break;
-        case 8: st = bq_fit<8>(y, n, p, q, I, x0, x, &nev); break;
+        case 2: st = bq_fit_k<2, WAVE>(y, n, p, q, I, x0, x, &nev, smem); break;
+        case 3: st = bq_fit_k<3, WAVE>(y, n, p, q, I, x0, x, &nev, smem); break;
+        case 4: st = bq_fit_k<4, WAVE>(y, n, p, q, I, x0, x, &nev, smem); break;
+        case 5: st = bq_fit_k<5, WAVE>(y, n, p, q, I, x0, x, &nev, smem); break;
+        case 6: st = bq_fit_k<6, WAVE>(y, n, p, q, I, x0, x, &nev, smem); break;
+        case 7: st = bq_fit_k<7, WAVE>(y, n, p, q, I, x0, x, &nev, smem); break;
+        case 8: st = bq_fit_k<8, WAVE>(y, n, p, q, I, x0, x, &nev, smem); break;
         default: st = ARIMA_ST_TOO_FEW_PARAMS; break;   /* k < 2: BOBYQAOptimizer.setup */
         }
     }
     const bool ok = st == ARIMA_ST_OK;
+    const double llv = ok ? bq_css_ll(y, n, p, q, I, x) : __builtin_nan("");
+    const uint8_t fl = ok ? bq_model_flags(x, p, q, I) : (uint8_t)0;
+    if (WAVE && threadIdx.x != 0) return;
     for (int j = 0; j < k; ++j) coef[base + j] = ok ? x[j] : __builtin_nan("");
-    ll[r] = ok ? bq_css_ll(y, n, p, q, I, x) : __builtin_nan("");
+    ll[r] = llv;
     status[r] = st;
-    flags[r] = ok ? bq_model_flags(x, p, q, I) : (uint8_t)0;
+    flags[r] = fl;
 }
 
 int launch_bobyqa_refit_round(const double *rows, int64_t ld, int n, const int32_t *lists, int64_t N,
                               const int64_t *off, int64_t total, const double *init, const int32_t *init_status,
                               int32_t *list, unsigned *count, double *coef, double *ll, int32_t *status,
-                              uint8_t *flags, hipStream_t s) {
+                              uint8_t *flags, bool wave, hipStream_t s) {
     if (total == 0) return ARIMA_OK;
     if (hipMemsetAsync(count, 0, sizeof(unsigned), s) != hipSuccess) return ARIMA_E_DEVICE;
     const dim3 grid((unsigned)((total + 63) / 64));
     hipLaunchKernelGGL(k_af_refit_list, grid, dim3(64), 0, s, status, total, off, list, count);
-    hipLaunchKernelGGL(k_bobyqa_refit_rows, grid, dim3(64), 0, s, rows, ld, n, lists, N, off, list, count, init,
-                       init_status, coef, ll, status, flags);
+    if (wave)
+        hipLaunchKernelGGL(k_bobyqa_refit_rows<true>, dim3((unsigned)total), dim3(64), 0, s, rows, ld, n, lists, N,
+                           off, list, count, init, init_status, coef, ll, status, flags);
+    else
+        hipLaunchKernelGGL(k_bobyqa_refit_rows<false>, grid, dim3(64), 0, s, rows, ld, n, lists, N, off, list, count,
+                           init, init_status, coef, ll, status, flags);
     return hipGetLastError() == hipSuccess ? ARIMA_OK : ARIMA_E_DEVICE;
 }
 
 int launch_bobyqa_fit(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, const double *init,
                       const int32_t *init_status, const int32_t *refit_status, double *coef_out, double *ll_out,
-                      int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
+                      int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out, bool wave,
                       hipStream_t s) {
     if (N == 0) return ARIMA_OK;
     if (p > 5 || q > 5 || I + p + q > BQ_KMAX) return ARIMA_E_UNSUPPORTED;
-    // one instantiation per dimension k = I + p + q: Powell's loops get compile-time bounds, so they unroll and the
-    // short vectors (d, xopt, gopt, ...) live in registers instead of the lane's scratch
-    const dim3 grid((unsigned)((N + 63) / 64));
+    // one instantiation per dimension k = I + p + q: Powell's loops get compile-time bounds
+    const dim3 grid_lane((unsigned)((N + 63) / 64)), grid_wave((unsigned)N);
 #define BQ_LAUNCH(K)                                                                                                  \
     case K:                                                                                                           \
-        hipLaunchKernelGGL(k_bobyqa_fit<K>, grid, dim3(64), 0, s, y, ld, n, N, p, q, I, init, init_status,            \
-                           refit_status, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out);            \
+        if (wave)                                                                                                     \
+            hipLaunchKernelGGL((k_bobyqa_fit<K, true>), grid_wave, dim3(64), 0, s, y, ld, n, N, p, q, I, init,        \
+                               init_status, refit_status, coef_out, ll_out, status_out, n_eval_out, n_grad_out,       \
+                               flags_out);                                                                            \
+        else                                                                                                          \
+            hipLaunchKernelGGL((k_bobyqa_fit<K, false>), grid_lane, dim3(64), 0, s, y, ld, n, N, p, q, I, init,       \
+                               init_status, refit_status, coef_out, ll_out, status_out, n_eval_out, n_grad_out,       \
+                               flags_out);                                                                            \
         break;
     switch (I + p + q) {
         BQ_LAUNCH(0) BQ_LAUNCH(1) BQ_LAUNCH(2) BQ_LAUNCH(3) BQ_LAUNCH(4) BQ_LAUNCH(5) BQ_LAUNCH(6) BQ_LAUNCH(7)

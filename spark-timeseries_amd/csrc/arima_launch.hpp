@@ -92,7 +92,7 @@ int launch_af_finish(int64_t N, const AfSeries *st, const double *best_coef, int
 // series whose css-cgd status there is an optimizer exception (autoFit's fitTryBothStrategies) are refitted in place
 int launch_bobyqa_fit(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, const double *init,
                       const int32_t *init_status, const int32_t *refit_status, double *coef_out, double *ll_out,
-                      int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
+                      int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out, bool wave,
                       hipStream_t s);
 
 // autoFit: the css-bobyqa retries of a whole round (every order's rows whose css-cgd fit threw in the optimizer), one
@@ -101,7 +101,7 @@ int launch_bobyqa_fit(const double *y, int64_t ld, int n, int64_t N, int p, int 
 int launch_bobyqa_refit_round(const double *rows, int64_t ld, int n, const int32_t *lists, int64_t N,
                               const int64_t *off, int64_t total, const double *init, const int32_t *init_status,
                               int32_t *list, unsigned *count, double *coef, double *ll, int32_t *status,
-                              uint8_t *flags, hipStream_t s);
+                              uint8_t *flags, bool wave, hipStream_t s);
 
 int hr_shape_status_host(int n, int p, int q, int I);
 int ar_shape_status_host(int n, int p, int I);

@@ -93,6 +93,7 @@ struct SliceSlot {
 constexpr int kMaxSearchLanes = sts::kSearchMaxLanes;
 constexpr int kMaxD = 16;
 constexpr int kMaxPipeline = 8;
+constexpr int64_t kBobyqaWaveMaxN = 4096;     // css-bobyqa fits up to this many series: a wave per series
 
 // One fit context: what a fit call needs for itself (stream, differenced-series workspace, HR init, kernel counters,
 // timing events, pinned counter copy, host-path staging). Fit calls rotate over h->pipeline contexts, so with
@@ -166,6 +167,13 @@ struct arima_handle {
     // else 0 (alone it is 25.2 vs 26.9 ms at C2)
     int hr_grid = -1;
     int row_pad = 0;               // doubles (multiple of 16) added to the differenced rows' stride
+    // css-bobyqa layout: 1 = a wave per series (state in LDS), 0 = a lane per series, -1 (default) = a wave per series
+    // for autoFit's retries and for fits of <= kBobyqaWaveMaxN series, else a lane per series. Bit-identical; measured
+    // on C2 series: 1 024 fits 0.20 (wave) vs 0.62 s (lane), 16 384 fits ~1.6 (8 x the 1 024-series wave time: 2 048
+    // series resident) vs 0.96 s, 65 536 fits 3.56 vs 1.79 s, autoFit of 65 536 series 11.98 vs 35.0 s
+    // (profiles/r05/q_wave, r_occ2, g_tmpl). An objective parallel in time over the row in LDS (css_pit_lds) was
+    // slower in this kernel: autoFit 19.3 s, 1 024 fits 0.27 s (s_pit)
+    int bobyqa_wave = -1;
     int64_t last_express = 0;
     int64_t last_grid = 0;
     int search_lanes = 8;          // concurrent fits of the order search (2/4/8: 1269/1303/1408 series/s, profiles/r02/g_c5)
@@ -536,6 +544,7 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
     if (!h || !name) return ARIMA_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
     if (!strcmp(name, "smear")) { h->smear = value ? 1 : 0; return ARIMA_OK; }
+    if (!strcmp(name, "bobyqa_wave")) { h->bobyqa_wave = value < 0 ? -1 : (value ? 1 : 0); return ARIMA_OK; }
     if (!strcmp(name, "row_pad")) {                 // doubles, rounded up to whole 128-B lines
         h->row_pad = (int)round_up(std::min<int64_t>(4096, std::max<int64_t>(0, value)), 16);
         return ARIMA_OK;
@@ -587,7 +596,7 @@ int arima_get_option(const arima_handle *hc, const char *name, int64_t *value) {
         {"smear", h->smear}, {"express_blocks", h->express_blocks}, {"grid_blocks", h->grid_blocks_override},
         {"search_lanes", h->search_lanes}, {"fit_pipeline", h->pipeline}, {"host_pipeline", h->host_pipeline},
         {"host_chunk", h->host_chunk}, {"fit_slice_bytes", h->fit_slice_bytes}, {"express_ring", h->express_ring},
-        {"hr_grid", h->hr_grid}, {"row_pad", h->row_pad}, {"merge_live", h->merge_live},
+        {"hr_grid", h->hr_grid}, {"row_pad", h->row_pad}, {"bobyqa_wave", h->bobyqa_wave}, {"merge_live", h->merge_live},
         {"search_express_blocks", h->search_express_blocks}, {"donate_evals", h->donate_evals},
         {"call_slices", h->call_slices}, {"call_slice_min", h->call_slice_min},
         {"donate_evals_drained", h->donate_evals_drained}};
@@ -734,7 +743,9 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
     if (ev_mid) HIPCHK(h, hipEventRecord(ev_mid, s));
     if (method == ARIMA_METHOD_CSS_BOBYQA && k > 0) {           // fitWithCSSBOBYQA, ARIMA.scala:106, :130-160
         RCCHK(h, sts::launch_bobyqa_fit(y, ldn, n, N, p, q, I, init, init_status, nullptr, d_coef, d_ll, d_status,
-                                        d_neval, d_ngrad, d_flags, s), "bobyqa_fit");
+                                        d_neval, d_ngrad, d_flags,
+                                        h->bobyqa_wave < 0 ? N <= kBobyqaWaveMaxN : h->bobyqa_wave != 0, s),
+              "bobyqa_fit");
         return ARIMA_OK;
     }
     if (method != ARIMA_METHOD_CSS_CGD || k == 0) {
@@ -1787,7 +1798,7 @@ static int autofit_locked(arima_handle *h, const double *d_series, int64_t N, in
                                                 h->af_hrst.as<int32_t>(), h->af_rlist.as<int32_t>(),
                                                 h->af_rcount.as<unsigned>(), h->af_coef.as<double>(),
                                                 h->af_ll.as<double>(), h->af_status.as<int32_t>(),
-                                                h->af_flags.as<uint8_t>(), s), "bobyqa refit");
+                                                h->af_flags.as<uint8_t>(), h->bobyqa_wave != 0, s), "bobyqa refit");
         RCCHK(h, sts::launch_af_update(N, st, h->af_off.as<int64_t>(), h->af_coef.as<double>(), h->af_ll.as<double>(),
                                        h->af_status.as<int32_t>(), h->af_flags.as<uint8_t>(), h->af_best.as<double>(),
                                        max_p, max_q, s), "autofit update");

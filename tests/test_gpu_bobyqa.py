@@ -54,3 +54,33 @@ def test_bobyqa_user_init_and_device_entry_point(engine):
     res = {k: v.cpu().numpy() for k, v in o.items()}
     res["coef"] = res["coef"].reshape(N, 3)
     check_fit(res, _expected(s.cpu().numpy(), 1, 0, 1, 1), "bobyqa_device")
+
+
+def test_bobyqa_layouts_are_transparent(engine):
+    # the lane-per-series and wave-per-series kernels (option bobyqa_wave 0 / 1; the default picks by batch size and
+    # uses the wave layout for autoFit's retries) run the same operations: outputs bit-identical, for direct fits of
+    # several dimensions and for autoFit's retries; a subsample against the oracle
+    import torch
+    from test_gpu_autofit import check_autofit
+    N, T = 512, 1024
+    s = torch.empty((N, T), dtype=torch.float64, device="cuda")
+    engine.sample_device(s.data_ptr(), N, T, T, 2, 1, 2, 1, [8.2, 0.2, 0.5, 0.3, 0.1], 0.05, 4711, 0)
+    engine.synchronize()
+    host = s.cpu().numpy()
+    prev = engine.get_option("bobyqa_wave")
+    try:
+        for (p, q, I) in ((2, 2, 1), (1, 1, 0), (4, 2, 1)):
+            res = {}
+            for wave in (0, 1):
+                engine.set_option("bobyqa_wave", wave)
+                res[wave] = engine.fit_batch(host, p, 1, q, bool(I), 1)
+            check_fit(res[1], res[0], f"layouts_{p}{q}{I}")
+        idx = np.arange(0, N, 61)
+        check_fit({k: v[idx] for k, v in res[1].items()}, _expected(host[idx], 4, 1, 2, 1), "layouts_oracle")
+        af = {}
+        for wave in (0, 1):
+            engine.set_option("bobyqa_wave", wave)
+            af[wave] = engine.autofit(host[:128], 5, 2, 5)
+        check_autofit(af[1], af[0], "autofit_layouts")
+    finally:
+        engine.set_option("bobyqa_wave", prev)
