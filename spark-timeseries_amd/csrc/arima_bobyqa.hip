@@ -30,8 +30,28 @@ template <int NN>
 struct BqState {
     static constexpr int N1 = NN > 0 ? NN : 1, NPT = 2 * N1 + 1, NDIM = NPT + N1;
     double xbase[N1], xpt[NPT * N1], fval[NPT], xopt[N1], gopt[N1], hq[N1 * (N1 + 1) / 2], pq[NPT], bmat[NDIM * N1],
-        zmat[NPT * N1], sl[N1], su[N1], xnew[N1], xalt[N1], d[N1], vlag[NDIM], w[3 * NDIM], x[N1], tw[5 * N1];
+        zmat[NPT * N1], sl[N1], su[N1], xnew[N1], xalt[N1], d[N1], vlag[NDIM], w[3 * NDIM], x[N1], tw[5 * N1],
+        par[2 * NDIM];                             // the wave layout's per-index temporaries
 };
+
+// for i in [0, count): f(i), independent bodies. Wave layout: lane i (i < count, strided by 64) runs body i, then
+// the wave's LDS writes are complete before any lane reads them (one wave per workgroup: a cheap barrier). Lane
+// layout: the serial loop. Each body runs the serial code's operations for its index in their order, so every
+// value is the serial loop's bit for bit.
+template <bool WAVE, class F>
+__device__ __forceinline__ void bq_par(int count, F &&f) {
+    if constexpr (WAVE) {
+        for (int i = (int)(threadIdx.x & 63); i < count; i += 64) f(i);
+        __syncthreads();
+    } else {
+        for (int i = 0; i < count; i++) f(i);
+    }
+}
+
+template <bool WAVE>
+__device__ __forceinline__ void bq_sync() {        // uniform LDS writes before other lanes read them
+    if constexpr (WAVE) __syncthreads();
+}
 
 // logLikelihoodCSSARMA (ARIMA.scala:430-445, iterateARMA :581-618, updateMAErrors :544-554) at runtime orders
 // p, q <= 5: the operations of css_pass in the same order (dest = 0 + I * c0, + AR lags, + MA terms; the ascending
@@ -148,11 +168,11 @@ __device__ __forceinline__ double bq_jmin(double a, double b) {
 }
 
 /* ---- TRSBOX (trust-region step of the quadratic model, bound tests inactive) ---------------------------- */
-template <int NN>
+template <int NN, bool WAVE = false>
 __device__ __forceinline__ void bq_trsbox(const double *xpt, const double *xopt, const double *gopt, const double *hq,
                       const double *pq, const double *sl, const double *su, double delta, double *xnew, double *d,
                       double *gnew, double *xbdi, double *s, double *hs, double *hred, double *dsq_out,
-                      double *crvmin_out) {
+                      double *crvmin_out, double *par) {
     constexpr int n = NN, npt = 2 * NN + 1;
     int iterc = 0, nact = 0, itermax = 0, itcsav = 0, iact = 0, isav = 0, iu = 0;
     double beta = 0, stepsq = 0, gredsq = 0, delsq, qred, crvmin, resid, ds, shs, temp, blen, stplen, sdec, ggsav = 0;
@@ -397,12 +417,29 @@ __device__ __forceinline__ void bq_trsbox(const double *xpt, const double *xopt,
                     ih++;
                 }
             }
-            for (int k = 0; k < npt; k++) {
-                if (pq[k] != 0.0) {
-                    temp = 0.0;
-                    for (int j = 0; j < n; j++) temp = temp + XPT(k, j) * s[j];
-                    temp = temp * pq[k];
-                    for (int i = 0; i < n; i++) hs[i] = hs[i] + temp * XPT(k, i);
+            bq_sync<WAVE>();
+            if constexpr (WAVE) {                // per-point scalars by lane k, then hs[i] folded over k by lane i
+                bq_par<true>(npt, [&](int k) {
+                    if (pq[k] != 0.0) {
+                        double t = 0.0;
+                        for (int j = 0; j < n; j++) t = t + XPT(k, j) * s[j];
+                        par[k] = t * pq[k];
+                    }
+                });
+                bq_par<true>(n, [&](int i) {
+                    double h = hs[i];
+                    for (int k = 0; k < npt; k++)
+                        if (pq[k] != 0.0) h = h + par[k] * XPT(k, i);
+                    hs[i] = h;
+                });
+            } else {
+                for (int k = 0; k < npt; k++) {
+                    if (pq[k] != 0.0) {
+                        temp = 0.0;
+                        for (int j = 0; j < n; j++) temp = temp + XPT(k, j) * s[j];
+                        temp = temp * pq[k];
+                        for (int i = 0; i < n; i++) hs[i] = hs[i] + temp * XPT(k, i);
+                    }
                 }
             }
             if (crvmin != 0.0) { state = 50; break; }
@@ -587,9 +624,9 @@ __device__ __forceinline__ void bq_altmov(const double *xpt, const double *xopt,
 }
 
 /* ---- UPDATE (BMAT and ZMAT after moving the KNEW-th interpolation point) ---------------------------------- */
-template <int NN>
+template <int NN, bool WAVE = false>
 __device__ __forceinline__ void bq_update(double *bmat, double *zmat, double *vlag, double beta, double denom, int knew,
-                      double *w) {
+                      double *w, double *par) {
     constexpr int n = NN, npt = 2 * NN + 1;
     const int nptm = npt - n - 1;
     double ztest = 0.0, temp, tempa, tempb, alpha, tau;
@@ -601,37 +638,48 @@ __device__ __forceinline__ void bq_update(double *bmat, double *zmat, double *vl
             temp = sqrt(ZMAT(knew, 0) * ZMAT(knew, 0) + ZMAT(knew, j) * ZMAT(knew, j));
             tempa = ZMAT(knew, 0) / temp;
             tempb = ZMAT(knew, j) / temp;
-            for (int i = 0; i < npt; i++) {
-                temp = tempa * ZMAT(i, 0) + tempb * ZMAT(i, j);
-                ZMAT(i, j) = tempa * ZMAT(i, j) - tempb * ZMAT(i, 0);
-                ZMAT(i, 0) = temp;
-            }
+            const double ta = tempa, tb = tempb;
+            bq_par<WAVE>(npt, [&](int i) {
+                const double t = ta * ZMAT(i, 0) + tb * ZMAT(i, j);
+                ZMAT(i, j) = ta * ZMAT(i, j) - tb * ZMAT(i, 0);
+                ZMAT(i, 0) = t;
+            });
         }
         ZMAT(knew, j) = 0.0;
+        bq_sync<WAVE>();
     }
-    for (int i = 0; i < npt; i++) w[i] = ZMAT(knew, 0) * ZMAT(i, 0);
+    bq_par<WAVE>(npt, [&](int i) { w[i] = ZMAT(knew, 0) * ZMAT(i, 0); });
     alpha = w[knew];
     tau = vlag[knew];
+    bq_sync<WAVE>();
     vlag[knew] = vlag[knew] - 1.0;
     temp = sqrt(denom);
     tempb = ZMAT(knew, 0) / temp;
     tempa = tau / temp;
-    for (int i = 0; i < npt; i++) ZMAT(i, 0) = tempa * ZMAT(i, 0) - tempb * vlag[i];
+    bq_sync<WAVE>();
+    {
+        const double ta = tempa, tb = tempb;
+        bq_par<WAVE>(npt, [&](int i) { ZMAT(i, 0) = ta * ZMAT(i, 0) - tb * vlag[i]; });
+    }
     for (int j = 0; j < n; j++) {
         const int jp = npt + j;
-        w[jp] = BMAT(knew, j);
-        tempa = (alpha * vlag[jp] - tau * w[jp]) / denom;
-        tempb = (-beta * w[jp] - tau * vlag[jp]) / denom;
-        for (int i = 0; i <= jp; i++) {
-            BMAT(i, j) = BMAT(i, j) + tempa * vlag[i] + tempb * w[i];
+        const double wj = BMAT(knew, j);
+        bq_sync<WAVE>();
+        w[jp] = wj;
+        const double ta = (alpha * vlag[jp] - tau * wj) / denom;
+        const double tb = (-beta * wj - tau * vlag[jp]) / denom;
+        bq_sync<WAVE>();
+        bq_par<WAVE>(jp + 1, [&](int i) {
+            BMAT(i, j) = BMAT(i, j) + ta * vlag[i] + tb * w[i];
             if (i >= npt) BMAT(jp, i - npt) = BMAT(i, j);
-        }
+        });
     }
+    (void)par;
 }
 
 /* ---- BOBYQA driver + PRELIM + BOBYQB, unbounded, npt = 2n + 1 ------------------------------------------- *
  * Returns ARIMA_ST_*; x (in: the initial point, out: the optimum), n_eval_out = objective evaluations. */
-template <int NN>
+template <int NN, bool WAVE = false>
 __device__ __forceinline__ int bq_fit(const double *y, int len, int p, int q, int I, const double *x0, double *x_out,
                                       int *n_eval_out, BqState<NN> &S) {
     constexpr int n = NN;                                      /* = I + p + q (the launcher's instantiation) */
@@ -763,8 +811,8 @@ __device__ __forceinline__ int bq_fit(const double *y, int len, int p, int q, in
             }
             /* fallthrough */
         case 60:
-            bq_trsbox<NN>(xpt, xopt, gopt, hq, pq, sl, su, delta, xnew, d, tw, tw + n, tw + 2 * n, tw + 3 * n,
-                      tw + 4 * n, &dsq, &crvmin);
+            bq_trsbox<NN, WAVE>(xpt, xopt, gopt, hq, pq, sl, su, delta, xnew, d, tw, tw + n, tw + 2 * n, tw + 3 * n,
+                      tw + 4 * n, &dsq, &crvmin, S.par);
             dnorm = bq_jmin(delta, sqrt(dsq));
             if (dnorm < 0.5 * rho) {
                 ntrits = -1;
@@ -863,7 +911,8 @@ __device__ __forceinline__ int bq_fit(const double *y, int len, int p, int q, in
             for (int i = 0; i < n; i++) d[i] = xnew[i] - xopt[i];
             /* fallthrough */
         case 230: {
-            for (int k = 0; k < npt; k++) {
+            bq_sync<WAVE>();
+            bq_par<WAVE>(npt, [&](int k) {
                 double suma = 0.0, sumb = 0.0, sum = 0.0;
                 for (int j = 0; j < n; j++) {
                     suma = suma + XPT(k, j) * d[j];
@@ -873,29 +922,48 @@ __device__ __forceinline__ int bq_fit(const double *y, int len, int p, int q, in
                 w[k] = suma * (0.5 * suma + sumb);
                 vlag[k] = sum;
                 w[npt + k] = suma;
-            }
+            });
             beta = 0.0;
             for (int jj = 0; jj < nptm; jj++) {
                 double sum = 0.0;
                 for (int k = 0; k < npt; k++) sum = sum + ZMAT(k, jj) * w[k];
                 beta = beta - sum * sum;
-                for (int k = 0; k < npt; k++) vlag[k] = vlag[k] + sum * ZMAT(k, jj);
+                bq_par<WAVE>(npt, [&](int k) { vlag[k] = vlag[k] + sum * ZMAT(k, jj); });
             }
             dsq = 0.0;
             double bsum = 0.0, dx = 0.0;
-            for (int j = 0; j < n; j++) {
-                dsq = dsq + d[j] * d[j];
-                double sum = 0.0;
-                for (int k = 0; k < npt; k++) sum = sum + w[k] * BMAT(k, j);
-                bsum = bsum + sum * d[j];
-                const int jp = npt + j;
-                for (int i = 0; i < n; i++) sum = sum + BMAT(jp, i) * d[i];
-                vlag[jp] = sum;
-                bsum = bsum + sum * d[j];
-                dx = dx + d[j] * xopt[j];
+            if constexpr (WAVE) {                // the column sums by lane j, then the three folds over j in order
+                double *par = S.par;
+                bq_par<true>(n, [&](int j) {
+                    double sum = 0.0;
+                    for (int k = 0; k < npt; k++) sum = sum + w[k] * BMAT(k, j);
+                    par[j] = sum;
+                    const int jp = npt + j;
+                    for (int i = 0; i < n; i++) sum = sum + BMAT(jp, i) * d[i];
+                    vlag[jp] = sum;
+                });
+                for (int j = 0; j < n; j++) {
+                    dsq = dsq + d[j] * d[j];
+                    bsum = bsum + par[j] * d[j];
+                    bsum = bsum + vlag[npt + j] * d[j];
+                    dx = dx + d[j] * xopt[j];
+                }
+            } else {
+                for (int j = 0; j < n; j++) {
+                    dsq = dsq + d[j] * d[j];
+                    double sum = 0.0;
+                    for (int k = 0; k < npt; k++) sum = sum + w[k] * BMAT(k, j);
+                    bsum = bsum + sum * d[j];
+                    const int jp = npt + j;
+                    for (int i = 0; i < n; i++) sum = sum + BMAT(jp, i) * d[i];
+                    vlag[jp] = sum;
+                    bsum = bsum + sum * d[j];
+                    dx = dx + d[j] * xopt[j];
+                }
             }
             beta = dx * dx + dsq * (xoptsq + dx + dx + 0.5 * dsq) + beta - bsum;
             vlag[kopt] = vlag[kopt] + 1.0;
+            bq_sync<WAVE>();
             if (ntrits == 0) {
                 denom = vlag[knew] * vlag[knew] + alpha * beta;
                 if (denom < cauchy && cauchy > 0.0) {
@@ -918,14 +986,32 @@ __device__ __forceinline__ int bq_fit(const double *y, int len, int p, int q, in
                 // KNEW = 0 in Powell's 1-based code; a 0-based translation resets to index 0 (a NaN model never
                 // replaces it, and the point index stays in range)
                 knew = 0;
+                if constexpr (WAVE) {            // every point's den and weight by lane k (the scan below reads them)
+                    double *par = S.par;
+                    const double bt = beta;
+                    bq_par<true>(npt, [&](int k) {
+                        double hdiag = 0.0;
+                        for (int jj = 0; jj < nptm; jj++) hdiag = hdiag + ZMAT(k, jj) * ZMAT(k, jj);
+                        par[k] = bt * hdiag + vlag[k] * vlag[k];
+                        double ds2 = 0.0;
+                        for (int j = 0; j < n; j++) ds2 = ds2 + (XPT(k, j) - xopt[j]) * (XPT(k, j) - xopt[j]);
+                        par[BqState<NN>::NDIM + k] = bq_jmax(1.0, (ds2 / delsq) * (ds2 / delsq));
+                    });
+                }
                 for (int k = 0; k < npt; k++) {
                     if (k == kopt) continue;
-                    double hdiag = 0.0;
-                    for (int jj = 0; jj < nptm; jj++) hdiag = hdiag + ZMAT(k, jj) * ZMAT(k, jj);
-                    const double den = beta * hdiag + vlag[k] * vlag[k];
-                    double ds2 = 0.0;
-                    for (int j = 0; j < n; j++) ds2 = ds2 + (XPT(k, j) - xopt[j]) * (XPT(k, j) - xopt[j]);
-                    const double temp = bq_jmax(1.0, (ds2 / delsq) * (ds2 / delsq));
+                    double den, temp;
+                    if constexpr (WAVE) {
+                        den = S.par[k];
+                        temp = S.par[BqState<NN>::NDIM + k];
+                    } else {
+                        double hdiag = 0.0;
+                        for (int jj = 0; jj < nptm; jj++) hdiag = hdiag + ZMAT(k, jj) * ZMAT(k, jj);
+                        den = beta * hdiag + vlag[k] * vlag[k];
+                        double ds2 = 0.0;
+                        for (int j = 0; j < n; j++) ds2 = ds2 + (XPT(k, j) - xopt[j]) * (XPT(k, j) - xopt[j]);
+                        temp = bq_jmax(1.0, (ds2 / delsq) * (ds2 / delsq));
+                    }
                     if (temp * den > scaden) {
                         scaden = temp * den;
                         knew = k;
@@ -982,13 +1068,31 @@ __device__ __forceinline__ int bq_fit(const double *y, int len, int p, int q, in
                     const double delsq = delta * delta;
                     double scaden = 0.0, biglsq = 0.0;
                     knew = 0;
+                    if constexpr (WAVE) {
+                        double *par = S.par;
+                        const double bt = beta;
+                        bq_par<true>(npt, [&](int k) {
+                            double hdiag = 0.0;
+                            for (int jj = 0; jj < nptm; jj++) hdiag = hdiag + ZMAT(k, jj) * ZMAT(k, jj);
+                            par[k] = bt * hdiag + vlag[k] * vlag[k];
+                            double ds2 = 0.0;
+                            for (int j = 0; j < n; j++) ds2 = ds2 + (XPT(k, j) - xnew[j]) * (XPT(k, j) - xnew[j]);
+                            par[BqState<NN>::NDIM + k] = bq_jmax(1.0, (ds2 / delsq) * (ds2 / delsq));
+                        });
+                    }
                     for (int k = 0; k < npt; k++) {
-                        double hdiag = 0.0;
-                        for (int jj = 0; jj < nptm; jj++) hdiag = hdiag + ZMAT(k, jj) * ZMAT(k, jj);
-                        const double den = beta * hdiag + vlag[k] * vlag[k];
-                        double ds2 = 0.0;
-                        for (int j = 0; j < n; j++) ds2 = ds2 + (XPT(k, j) - xnew[j]) * (XPT(k, j) - xnew[j]);
-                        const double temp = bq_jmax(1.0, (ds2 / delsq) * (ds2 / delsq));
+                        double den, temp;
+                        if constexpr (WAVE) {
+                            den = S.par[k];
+                            temp = S.par[BqState<NN>::NDIM + k];
+                        } else {
+                            double hdiag = 0.0;
+                            for (int jj = 0; jj < nptm; jj++) hdiag = hdiag + ZMAT(k, jj) * ZMAT(k, jj);
+                            den = beta * hdiag + vlag[k] * vlag[k];
+                            double ds2 = 0.0;
+                            for (int j = 0; j < n; j++) ds2 = ds2 + (XPT(k, j) - xnew[j]) * (XPT(k, j) - xnew[j]);
+                            temp = bq_jmax(1.0, (ds2 / delsq) * (ds2 / delsq));
+                        }
                         if (temp * den > scaden) {
                             scaden = temp * den;
                             knew = k;
@@ -1002,35 +1106,59 @@ __device__ __forceinline__ int bq_fit(const double *y, int len, int p, int q, in
                     }
                 }
             }
-            bq_update<NN>(bmat, zmat, vlag, beta, denom, knew, w);
+            bq_update<NN, WAVE>(bmat, zmat, vlag, beta, denom, knew, w, S.par);
             {
-                int ih = 0;
                 const double pqold = pq[knew];
+                bq_sync<WAVE>();
                 pq[knew] = 0.0;
-                for (int i = 0; i < n; i++) {
+                bq_sync<WAVE>();
+                bq_par<WAVE>(nh, [&](int ih) {   // hq[ih], ih = i (i + 1) / 2 + j, j <= i
+                    int i = 0;
+                    while ((i + 1) * (i + 2) / 2 <= ih) i++;
+                    const int j = ih - i * (i + 1) / 2;
                     const double temp = pqold * XPT(knew, i);
-                    for (int j = 0; j <= i; j++) {
-                        hq[ih] = hq[ih] + temp * XPT(knew, j);
-                        ih++;
+                    hq[ih] = hq[ih] + temp * XPT(knew, j);
+                });
+                bq_par<WAVE>(npt, [&](int k) {
+                    double pk = pq[k];
+                    for (int jj = 0; jj < nptm; jj++) {
+                        const double temp = diff * ZMAT(knew, jj);
+                        pk = pk + temp * ZMAT(k, jj);
                     }
-                }
-                for (int jj = 0; jj < nptm; jj++) {
-                    const double temp = diff * ZMAT(knew, jj);
-                    for (int k = 0; k < npt; k++) pq[k] = pq[k] + temp * ZMAT(k, jj);
-                }
+                    pq[k] = pk;
+                });
             }
             fval[knew] = f;
             for (int i = 0; i < n; i++) {
-                XPT(knew, i) = xnew[i];
-                w[i] = BMAT(knew, i);
+                const double xi = xnew[i], bi = BMAT(knew, i);
+                bq_sync<WAVE>();
+                XPT(knew, i) = xi;
+                w[i] = bi;
             }
-            for (int k = 0; k < npt; k++) {
-                double suma = 0.0;
-                for (int jj = 0; jj < nptm; jj++) suma = suma + ZMAT(knew, jj) * ZMAT(k, jj);
-                double sumb = 0.0;
-                for (int j = 0; j < n; j++) sumb = sumb + XPT(k, j) * xopt[j];
-                const double temp = suma * sumb;
-                for (int i = 0; i < n; i++) w[i] = w[i] + temp * XPT(k, i);
+            bq_sync<WAVE>();
+            if constexpr (WAVE) {                // per-point scalars by lane k, then w[i] folded over k by lane i
+                double *par = S.par;
+                bq_par<true>(npt, [&](int k) {
+                    double suma = 0.0;
+                    for (int jj = 0; jj < nptm; jj++) suma = suma + ZMAT(knew, jj) * ZMAT(k, jj);
+                    double sumb = 0.0;
+                    for (int j = 0; j < n; j++) sumb = sumb + XPT(k, j) * xopt[j];
+                    par[k] = suma * sumb;
+                });
+                bq_par<true>(n, [&](int i) {
+                    double wi = w[i];
+                    for (int k = 0; k < npt; k++) wi = wi + par[k] * XPT(k, i);
+                    w[i] = wi;
+                });
+            } else {
+                for (int k = 0; k < npt; k++) {
+                    double suma = 0.0;
+                    for (int jj = 0; jj < nptm; jj++) suma = suma + ZMAT(knew, jj) * ZMAT(k, jj);
+                    double sumb = 0.0;
+                    for (int j = 0; j < n; j++) sumb = sumb + XPT(k, j) * xopt[j];
+                    const double temp = suma * sumb;
+                    for (int i = 0; i < n; i++) w[i] = w[i] + temp * XPT(k, i);
+                }
             }
             for (int i = 0; i < n; i++) gopt[i] = gopt[i] + diff * w[i];
             if (f < fopt) {
@@ -1046,33 +1174,61 @@ __device__ __forceinline__ int bq_fit(const double *y, int len, int p, int q, in
                         ih++;
                     }
                 }
-                for (int k = 0; k < npt; k++) {
-                    double temp = 0.0;
-                    for (int j = 0; j < n; j++) temp = temp + XPT(k, j) * d[j];
-                    temp = pq[k] * temp;
-                    for (int i = 0; i < n; i++) gopt[i] = gopt[i] + temp * XPT(k, i);
+                bq_sync<WAVE>();
+                if constexpr (WAVE) {
+                    double *par = S.par;
+                    bq_par<true>(npt, [&](int k) {
+                        double temp = 0.0;
+                        for (int j = 0; j < n; j++) temp = temp + XPT(k, j) * d[j];
+                        par[k] = pq[k] * temp;
+                    });
+                    bq_par<true>(n, [&](int i) {
+                        double g = gopt[i];
+                        for (int k = 0; k < npt; k++) g = g + par[k] * XPT(k, i);
+                        gopt[i] = g;
+                    });
+                } else {
+                    for (int k = 0; k < npt; k++) {
+                        double temp = 0.0;
+                        for (int j = 0; j < n; j++) temp = temp + XPT(k, j) * d[j];
+                        temp = pq[k] * temp;
+                        for (int i = 0; i < n; i++) gopt[i] = gopt[i] + temp * XPT(k, i);
+                    }
                 }
             }
             if (ntrits > 0) {
-                for (int k = 0; k < npt; k++) {
+                bq_sync<WAVE>();
+                bq_par<WAVE>(npt, [&](int k) {
                     vlag[k] = fval[k] - fval[kopt];
                     w[k] = 0.0;
-                }
+                });
                 for (int j = 0; j < nptm; j++) {
                     double sum = 0.0;
                     for (int k = 0; k < npt; k++) sum = sum + ZMAT(k, j) * vlag[k];
-                    for (int k = 0; k < npt; k++) w[k] = w[k] + sum * ZMAT(k, j);
+                    bq_par<WAVE>(npt, [&](int k) { w[k] = w[k] + sum * ZMAT(k, j); });
                 }
-                for (int k = 0; k < npt; k++) {
+                bq_par<WAVE>(npt, [&](int k) {
                     double sum = 0.0;
                     for (int j = 0; j < n; j++) sum = sum + XPT(k, j) * xopt[j];
                     w[k + npt] = w[k];
                     w[k] = sum * w[k];
+                });
+                if constexpr (WAVE) {
+                    double *par = S.par;
+                    bq_par<true>(n, [&](int i) {
+                        double sum = 0.0;
+                        for (int k = 0; k < npt; k++) sum = sum + BMAT(k, i) * vlag[k] + XPT(k, i) * w[k];
+                        par[i] = sum;
+                    });
                 }
                 double gqsq = 0.0, gisq = 0.0;
                 for (int i = 0; i < n; i++) {
                     double sum = 0.0;
-                    for (int k = 0; k < npt; k++) sum = sum + BMAT(k, i) * vlag[k] + XPT(k, i) * w[k];
+                    if constexpr (WAVE) {
+                        sum = S.par[i];
+                    } else {
+                        for (int k = 0; k < npt; k++) sum = sum + BMAT(k, i) * vlag[k] + XPT(k, i) * w[k];
+                    }
                     if (xopt[i] == sl[i]) {
                         gqsq = gqsq + bq_jmin(0.0, gopt[i]) * bq_jmin(0.0, gopt[i]);
                         gisq = gisq + bq_jmin(0.0, sum) * bq_jmin(0.0, sum);
@@ -1237,7 +1393,7 @@ __global__ __launch_bounds__(64, WAVE ? kBqWaveOcc : 1) void k_bobyqa_fit(const 
     for (int j = 0; j < BQ_KMAX; ++j) x0[j] = j < k ? init[sid * k + j] : 0.0;
     if constexpr (WAVE) {
         __shared__ BqState<NN> S;
-        if (st == ARIMA_ST_OK) st = bq_fit<NN>(y + sid * ld, n, p, q, I, x0, x, &nev, S);
+        if (st == ARIMA_ST_OK) st = bq_fit<NN, true>(y + sid * ld, n, p, q, I, x0, x, &nev, S);
     } else {
         BqState<NN> S;
         if (st == ARIMA_ST_OK) st = bq_fit<NN>(y + sid * ld, n, p, q, I, x0, x, &nev, S);
@@ -1289,7 +1445,7 @@ template <int K, bool WAVE>
 __device__ __forceinline__ int bq_fit_k(const double *y, int n, int p, int q, int I, const double *x0, double *x,
                                         int *nev, double *smem) {
     if constexpr (WAVE) {
-        return bq_fit<K>(y, n, p, q, I, x0, x, nev, *reinterpret_cast<BqState<K> *>(smem));
+        return bq_fit<K, true>(y, n, p, q, I, x0, x, nev, *reinterpret_cast<BqState<K> *>(smem));
     } else {
         BqState<K> S;
         return bq_fit<K>(y, n, p, q, I, x0, x, nev, S);
