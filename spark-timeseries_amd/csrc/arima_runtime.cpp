@@ -183,13 +183,9 @@ struct arima_handle {
     // calls: 1 / 2 / 3 / 4 contexts 6.68 / 8.30 / 10.02 / 9.97 M series/s; one call alone 151 ms at 1, 162 ms at 3
     // (drained bulk waves leave instead of turning express) -- profiles/r05/k_defp
     int pipeline = 3;
-    // one device fit call cut into this many slices on as many fit contexts (option "call_slices"; 1 = off, the
-    // default; -1 = auto: 3 for a call of >= 3 x call_slice_min series at fit_pipeline 1 on the handle's own streams).
-    // The slices of ONE call overlap while calls stay ordered (the next call waits for every slice). Measured on the
-    // box's 4 hardware queues at C2 1M x 1024 (profiles/r05/c_af2/default_cs*.json): 1 / 2 / 3 / 4 slices 6.91 /
-    // 6.39 / 6.35 / 4.47 M series/s -- every slice ends with its own slowest series, so it stays off
-    int call_slices = 1;
-    int64_t call_slice_min = 262144;
+    // (Cutting ONE call into slices over several contexts was measured on the box's 4 queues at C2 1M x 1024 and
+    // removed: 1 / 2 / 3 / 4 slices 6.91 / 6.39 / 6.35 / 4.47 M series/s, every slice ends with its own slowest
+    // series; profiles/r05/c_af2/default_cs*.json.)
     int host_pipeline = 3;         // contexts the chunked host path rotates over
     int64_t host_chunk = 1 << 18;  // series per chunk of the host path (option "host_chunk")
     int64_t fit_slice_bytes = 0;   // differenced workspace of one device-fit slice (option "fit_slice_bytes"; 0: from free HBM)
@@ -570,11 +566,6 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
         h->search_lanes = (int)std::min<int64_t>(kMaxSearchLanes, std::max<int64_t>(1, value));
         return ARIMA_OK;
     }
-    if (!strcmp(name, "call_slices")) {
-        h->call_slices = (int)std::min<int64_t>(kMaxPipeline, std::max<int64_t>(-1, value));
-        return ARIMA_OK;
-    }
-    if (!strcmp(name, "call_slice_min")) { h->call_slice_min = std::max<int64_t>(1024, value); return ARIMA_OK; }
     if (!strcmp(name, "fit_pipeline")) {
         h->pipeline = (int)std::min<int64_t>(kMaxPipeline, std::max<int64_t>(1, value));
         return ARIMA_OK;
@@ -598,7 +589,6 @@ int arima_get_option(const arima_handle *hc, const char *name, int64_t *value) {
         {"host_chunk", h->host_chunk}, {"fit_slice_bytes", h->fit_slice_bytes}, {"express_ring", h->express_ring},
         {"hr_grid", h->hr_grid}, {"row_pad", h->row_pad}, {"bobyqa_wave", h->bobyqa_wave}, {"merge_live", h->merge_live},
         {"search_express_blocks", h->search_express_blocks}, {"donate_evals", h->donate_evals},
-        {"call_slices", h->call_slices}, {"call_slice_min", h->call_slice_min},
         {"donate_evals_drained", h->donate_evals_drained}};
     for (const auto &o : opts)
         if (!strcmp(name, o.n)) {
@@ -611,8 +601,9 @@ int arima_get_option(const arima_handle *hc, const char *name, int64_t *value) {
 // ---------------------------------------------------------------------------------------------------------
 // Ordering. A non-fit call waits (on the device, not the host) for every earlier call: the building blocks share
 // the handle's workspaces, and any call may read an earlier call's outputs. A fit call waits for the earlier
-// non-fit calls (e.g. the sampler that wrote its input) and for the previous call on its own context; with
-// fit_pipeline = 1 (the default) that is the previous fit, so calls run in issue order.
+// non-fit calls (e.g. the sampler that wrote its input), for the previous call on its own context and, with
+// fit_pipeline > 1 (default 3), for any in-flight fit whose buffers its own overlap (order_after_overlapping_fits);
+// with fit_pipeline = 1 the previous call on its context is the previous fit, so calls run in issue order.
 static void begin_call(arima_handle *h, hipStream_t s) {
     if (h->has_done) hipStreamWaitEvent(s, h->ev_done, 0);
     for (auto &c : h->fctx)
@@ -957,15 +948,6 @@ int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_se
         slice_bytes = std::max<int64_t>(1ll << 30, (int64_t)((free_b + held) / 10 * 6 / (size_t)std::max(P, 1)));
     }
     int64_t slice = std::max<int64_t>(1024, slice_bytes / (ldn * (int64_t)sizeof(double)) / 1024 * 1024);
-    // call slicing (fit_pipeline 1, the handle's streams): S slices of one call on S contexts
-    int S = 1;
-    if (P == 1 && !stream && n_series > 0) {
-        S = h->call_slices >= 2 ? h->call_slices
-                                : (h->call_slices < 0 && n_series >= 3 * h->call_slice_min ? 3 : 1);
-        S = std::min(S, kMaxPipeline);
-        if (S > 1) slice = std::min(slice, std::max<int64_t>(1024, (n_series + S - 1) / S));
-    }
-    const int PC = std::max(P, S);                 // contexts this call's slices rotate over
     if (n_series <= slice || T < 0 || ld < T || n_series < 0) {
         const int ci = (int)(h->fit_seq++ % (unsigned)P);
         FitCtx &c = h->fctx[ci];
@@ -994,10 +976,6 @@ int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_se
     h->slice_first = h->slot_seq % kSliceSlots;
     h->slice_n = 0;
     h->slice_acc = arima_fit_stats{};
-    if (P == 1 && PC > 1 && !stream && h->fctx[0].has_done)
-        // calls stay ordered: every context of this call starts after the previous fit call (whose end context 0's
-        // event marks at fit_pipeline 1), captured before slice 0 re-records that event
-        for (int j = 1; j < PC; ++j) HIPCHK(h, hipStreamWaitEvent(h->fctx[j].stream, h->fctx[0].ev_done, 0));
     for (int64_t j = 0; j < nslices; ++j) {
         const int sl = (int)(h->slot_seq++ % kSliceSlots);
         SliceSlot &ss = h->slot[sl];
@@ -1016,8 +994,7 @@ int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_se
         }
         ss.ps = PendingStats{};
         const int64_t f = j * slice, ns = std::min(slice, n_series - f);
-        // fit_pipeline P > 1: the next context in the rotation; call slicing at P = 1: context j % S
-        const int ci = P > 1 ? (int)(h->fit_seq++ % (unsigned)P) : (int)(j % PC);
+        const int ci = (int)(h->fit_seq++ % (unsigned)P);             // the next context in the rotation
         FitCtx &c = h->fctx[ci];
         hipStream_t s = stream ? (hipStream_t)stream : c.stream;
         begin_fit(h, c, s);
@@ -1029,21 +1006,14 @@ int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_se
                                   d_n_eval_out ? d_n_eval_out + f : nullptr, d_n_grad_out ? d_n_grad_out + f : nullptr,
                                   d_flags_out ? d_flags_out + f : nullptr), s);
         const int rc = fit_device_locked(
-            h, c, ci, PC, d_series + f * ld, ns, T, ld, p, d, q, include_intercept, method,
+            h, c, ci, P, d_series + f * ld, ns, T, ld, p, d, q, include_intercept, method,
             d_user_init ? d_user_init + f * k : nullptr, d_coef_out + f * k, d_css_ll_out + f, d_status_out + f,
             d_n_eval_out ? d_n_eval_out + f : nullptr, d_n_grad_out ? d_n_grad_out + f : nullptr,
-            d_flags_out ? d_flags_out + f : nullptr, s, PC > 1, sl);
+            d_flags_out ? d_flags_out + f : nullptr, s, P > 1, sl);
         HIPCHK(h, end_fit(c, s));
         if (ev_call) HIPCHK(h, hipEventRecord(ev_call, s));
         h->slice_n++;
         if (rc != ARIMA_OK) return rc;
-    }
-    if (P == 1 && PC > 1) {
-        // the call ends when every slice has: context 0 (the next call's, at fit_pipeline 1) waits for all of them
-        FitCtx &c0 = h->fctx[0];
-        for (int j = 1; j < PC; ++j)
-            if (h->fctx[j].has_done) HIPCHK(h, hipStreamWaitEvent(c0.stream, h->fctx[j].ev_done, 0));
-        HIPCHK(h, end_fit(c0, c0.stream));
     }
     return ARIMA_OK;
 }

@@ -1,6 +1,6 @@
 #!/bin/bash
 # The drop-in with the ABI's defaults (bench.py's default leg, box hardware queues) under option overrides:
-# OPTS="call_slices=1 call_slices=2" or OPTS="fit_pipeline=1 fit_pipeline=3" (one SPARKTS_OPTIONS value per run; STEPS
+# OPTS="fit_pipeline=1 fit_pipeline=3" (one SPARKTS_OPTIONS value per run; STEPS
 # consecutive asynchronous calls, default 5). Run ON the GPU box from the repo root after tools/gpu_session.sh (same OUT).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/r05/${TAG:-s}
