@@ -79,3 +79,20 @@ def test_autofit_device_entry_point_and_bounds(engine):
     check_autofit({k: v.cpu().numpy() for k, v in out.items()}, arr, "device entry point")
     with pytest.raises(Exception):
         engine.autofit(arr["series"], 6, 2, 5)                       # p <= 5 compiled
+
+
+def test_autofit_long_series_matches_oracle(engine):
+    # T = 3000: KPSS lag 12 (the register ring's longer reach), longer css-cgd fits and css-bobyqa retries on rows
+    # past the express path's parallel-in-time length; mixed I(0) / I(1) / I(2) series
+    rng = np.random.default_rng(2026)
+    N, T = 12, 3000
+    e = rng.standard_normal((N, T))
+    s = e.copy()
+    for t in range(1, T):
+        s[:, t] = 0.6 * s[:, t - 1] + e[:, t] + 0.3 * e[:, t - 1]
+    s[4:8] = np.cumsum(s[4:8], axis=1)
+    s[8:] = np.cumsum(np.cumsum(s[8:], axis=1), axis=1) * 0.01
+    r = engine.autofit(s, 5, 2, 5)
+    exp = [O.autofit(row, 5, 2, 5) for row in s]
+    check_autofit(r, {k: np.array([x[k] for x in exp]) for k in ("status", "order", "n_fits", "coef", "aic")},
+                  "long_T3000")
