@@ -69,3 +69,21 @@ def test_bench_two_ranks_on_one_gpu_checks_every_rank_against_the_oracle():
     assert par["oracle_rows"] >= 2 * 256 and par["bit_identical"] == par["oracle_rows"]
     assert par["every_rank_bit_identical"] and par["min_rank_fraction"] == 1.0 and par["vs_isolated"]
     assert line["cpu_baseline"] is None                     # the CPU baseline is timed at N = 1 only
+
+
+def test_bench_autofit_two_ranks_on_one_gpu_checks_every_rank():
+    # the autoFit line on two ranks (sharing GPU 0): each rank auto-fits its own shard and compares its first rows
+    # with oracle.autofit; the verdicts meet in the gloo reductions
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "0", "--config", "af",
+           "--series", "1024", "--steps", "1", "--warmup", "0", "--cpu-seconds", "4"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    par = line["parity"]
+    assert line["n_gpus"] == 2 and par["ranks_checked"] == 2
+    assert par["oracle_rows"] >= 2 and par["bit_identical"] == par["oracle_rows"] and par["every_rank_bit_identical"]
+    assert line["config"]["series_total"] == 2048
