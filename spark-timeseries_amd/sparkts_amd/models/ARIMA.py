@@ -231,6 +231,23 @@ class ARIMAModel:
         return self._eng.css_gradient(np.asarray(diffedy, dtype=np.float64)[None, :], self.p, self.q,
                                       self.has_intercept, self.coefficients)[0]
 
+    def sample(self, n, seed=None):
+        """sample (ARIMA.scala:655-678; python/sparkts/models/ARIMA.py:182-194): n values of this ARIMA(p, d, q)
+        process -- M copies of the intercept, the ARMA filter over N(0, 1) noise with the noise as the errors, the
+        prefix dropped, then inverseDifferencesOfOrderD(., d), in the reference's operation order. The reference
+        draws its noise from an unseeded JDKRandomGenerator; here it is Philox4x32-10 + Box-Muller
+        (arima_sample_batch_device) under `seed` (a fresh random one by default). Orders up to p, q <= 8."""
+        import torch
+        if seed is None:
+            seed = int.from_bytes(np.random.default_rng().bytes(8), "little")
+        n = int(n)
+        eng = self._eng
+        out = torch.empty((1, max(n, 1)), dtype=torch.float64, device=f"cuda:{eng.device}")
+        if n > 0:
+            eng.sample_device(out.data_ptr(), 1, n, n, self.p, self.d, self.q, self.has_intercept, self.coefficients,
+                              0.0, int(seed) & ((1 << 64) - 1), 0)
+        return out[0, :n].cpu().numpy()
+
     def forecast(self, ts, nfuture):
         """forecast (ARIMA.scala:696-764)."""
         return self._eng.forecast(np.asarray(ts, dtype=np.float64)[None, :], self.p, self.d, self.q,

@@ -199,6 +199,13 @@ def test_python_mirror_api(engine):
     assert np.array_equal(mb.coefficients, eb["coef"])
     with pytest.raises(ARIMA.TooManyEvaluationsException):
         ARIMA.fit_model(1, 0, 1, np.full(50, np.nan))
+    # ARIMAModel.sample: the device sampler with this model's coefficients (jitter 0), deterministic per seed
+    s1, s2 = m.sample(300, seed=5), m.sample(300, seed=5)
+    assert s1.shape == (300,) and np.array_equal(s1, s2) and np.all(np.isfinite(s1))
+    assert not np.array_equal(s1, m.sample(300, seed=6)) and m.sample(0).shape == (0,)
+    refit = ARIMA.fit_model(1, 0, 1, m.sample(5000, seed=11))
+    d = np.abs(refit.coefficients - m.coefficients)                      # a refit, ARIMASuite.scala:58-74 style:
+    assert d[0] < 1.0 and np.all(d[1:] < 0.1)                           # intercept within 1, the rest within 0.1
     from sparkts_amd import fit_arima_partition
     recs = [("a", arr["series"][0]), ("b", arr["series"][0][:200]), ("c", arr["series"][0])]
     out = list(fit_arima_partition(recs, 1, 0, 1))
