@@ -343,19 +343,39 @@ def oracle_row_parity(res, exp):
     return int(ok.sum())
 
 
-def end_to_end(eng, series, p, d, q, I):
-    """SURVEY.md 8(d)(ii): the same fit from the caller's (pageable) host memory through the blocking host entry
-    point arima_fit_batch -- chunked uploads overlapped with the fits of earlier chunks, results back through pinned
-    staging into the caller's arrays. One warm-up call on the first chunk sizes the staging buffers."""
+def end_to_end(eng, series, p, d, q, I, last, barrier, world, dist, max_over_ranks):
+    """SURVEY.md 8(d)(ii) / 8(e): the same fit from the caller's (pageable) host memory through the blocking host entry
+    point arima_fit_batch -- the rows copied by host threads into pinned blocks and DMA'd while the fits of earlier
+    chunks run, results back through pinned staging into the caller's arrays. Every rank runs it at once on its own
+    shard (barrier, max over ranks), so at N > 1 the line carries the host DRAM / PCIe contention of N GPUs. One
+    warm-up call on the first chunk sizes the staging buffers. The results must equal the device path's (the last
+    timed step) bit for bit on every row."""
+    import numpy as np
     host = series.cpu().numpy()
     eng.fit_batch(host[: 1 << 18], p, d, q, bool(I))
+    barrier()
     t0 = time.perf_counter()
     r = eng.fit_batch(host, p, d, q, bool(I))
     dt = time.perf_counter() - t0
-    return {"value": len(host) / dt, "unit": "series fitted/sec", "seconds": dt, "series": len(host),
-            "bytes_in": int(host.nbytes), "converged_fraction": float((r["status"] == 0).mean()),
-            "path": "arima_fit_batch: pageable host N x T -> HBM (chunks of 262144 over 3 fit contexts) -> "
-                    "difference/HR/CG fit -> pinned staging -> caller's arrays"}
+    barrier()
+    dt_max = max_over_ranks(dt, dist if world > 1 else None)
+    same = np.ones(len(host), dtype=bool)
+    for k, v in r.items():
+        ref = last[k].cpu().numpy()
+        a, b = (v.view(np.int64), ref.view(np.int64)) if v.dtype == np.float64 else (v, ref)
+        same &= (a == b).reshape(len(host), -1).all(axis=1)
+    from sparkts_amd.sharding import parity_over_ranks
+    par = parity_over_ranks(int(same.sum()), len(host), dist if world > 1 else None)
+    total = len(host) * world
+    return {"value": total / dt_max, "unit": "series fitted/sec", "seconds": dt_max, "series": total,
+            "n_ranks": world, "bytes_in": int(host.nbytes) * world, "GBps_in": host.nbytes * world / dt_max / 1e9,
+            "converged_fraction": float((r["status"] == 0).mean()),
+            "bit_identical_to_device_path": par["every_rank_bit_identical"], "rows_compared": par["oracle_rows"],
+            "rows_identical": par["bit_identical"],
+            "options": {n: eng.get_option(n) for n in ("host_chunk", "host_pipeline", "host_copy_threads")},
+            "path": "arima_fit_batch on every rank at once: pageable host N x T -> host threads -> pinned blocks -> "
+                    "DMA to HBM (chunks over 3 fit contexts) -> fused differencing / HR / CG fit -> pinned staging "
+                    "-> caller's arrays; value = all ranks' series / the slowest rank's time"}
 
 
 def main():
@@ -569,6 +589,8 @@ def main():
             log(f"[rank {rank}] PARITY: {rows_checked - rows_ok} of {rows_checked} oracle rows differ from the timed step")
     from sparkts_amd.sharding import parity_over_ranks
     node_parity = parity_over_ranks(rows_ok, rows_checked, dist if world > 1 else None)
+    # the drop-in's own path from host memory, every rank at once
+    e2e = end_to_end(eng, series, p, d, q, I, last, barrier, world, dist, max_over_ranks) if args.e2e else None
 
     if rank == 0:
         sha = build_sha()
@@ -645,8 +667,8 @@ def main():
         }
         if default_leg is not None:
             result["default_config"] = default_leg
-        if world == 1 and args.e2e:
-            result["end_to_end_host"] = end_to_end(eng, series, p, d, q, I)
+        if e2e is not None:
+            result["end_to_end_host"] = e2e
         parity = {"configuration": f"the last timed step: fit_pipeline {args.pipeline} on GPU_MAX_HW_QUEUES="
                                    f"{os.environ.get('GPU_MAX_HW_QUEUES')}",
                   "vs_isolated": iso_mismatch == 0, "isolated_mismatch_series": iso_mismatch,

@@ -19,7 +19,8 @@
  *     except fit calls under the "fit_pipeline" option (arima_set_option; default 3): consecutive
  *     arima_fit_batch_device calls rotate over P fit contexts and may run concurrently -- unless a call's
  *     buffers overlap an in-flight call's (it reads that call's outputs, writes its inputs, or writes the same
- *     outputs): then it waits for that call, so results always equal fit_pipeline 1's. Every non-fit call
+ *     outputs): then it waits for that call, whatever fit_pipeline is set to when it is issued, so results always
+ *     equal fit_pipeline 1's. Every non-fit call
  *     still waits for all earlier calls. arima_get_last_stats waits for the last call's device work.
  *     Host-buffer entry points block (arima_fit_batch pipelines its own chunks internally: "host_chunk",
  *     "host_pipeline").
@@ -131,7 +132,10 @@ int         arima_num_params(int p, int q, int include_intercept);
 int         arima_get_last_stats(const arima_handle *h, arima_fit_stats *out);
 /* Blocks until the device work of every call issued on the handle so far has finished. */
 int         arima_synchronize(arima_handle *h);
-/* Tuning knobs (not part of the reference contract): "smear" (Breeze reading at ARIMA.scala:526, default 1),
+/* Orders: p, q <= 5 run the order-specialised kernels, 5 < p, q <= 20 the runtime-order path (arima_generic.hip: the
+ * same results, not tuned); p or q > 20 return ARIMA_E_UNSUPPORTED, and so do css-bobyqa fits of more than 11
+ * parameters (the dimensions its kernels compile) and autoFit with max_p > 8 (its css-bobyqa retries).
+ * Tuning knobs (not part of the reference contract): "smear" (Breeze reading at ARIMA.scala:526, default 1),
  * "fit_pipeline" (fit contexts in rotation for *_device fits, 1..8, default 3), "host_chunk" / "host_pipeline"
  * (series per chunk and contexts of the chunked host path, default 262144 / 3), "express_blocks",
  * "grid_blocks", "search_lanes" (in-kernel scheduler and order-search concurrency), "hr_grid" (k_hr_init grid:
@@ -143,7 +147,10 @@ int         arima_synchronize(arima_handle *h);
  * series hands them to waves still running and exits, 0..64, 0 = off; results never depend on it),
  * "search_express_blocks" (express CUs of each concurrent order-search fit, default 0; -1 = as "express_blocks"),
  * "donate_evals" / "donate_evals_drained" (evaluations before a series may move to an express wave, before / after
- * the batch's work counter ran out; 0 = the kernel's 256 / 32). */
+ * the batch's work counter ran out; 0 = the kernel's 256 / 32), "fuse_diff" (1, default: device fits of d <= 1 read the
+ * caller's rows and difference them inside every pass; 0: through a k_difference workspace -- identical results),
+ * "autofit_slice" (autoFit series per slice of its workspaces, 0 = from free HBM), "host_copy_threads" (host threads
+ * that copy arima_fit_batch's rows into pinned blocks for the upload, default 8; 0 = upload from pageable memory). */
 int         arima_set_option(arima_handle *h, const char *name, int64_t value);
 /* Current value of a tuning knob (the names arima_set_option takes); ARIMA_E_INVALID_ARG for an unknown name. */
 int         arima_get_option(const arima_handle *h, const char *name, int64_t *value);
@@ -217,7 +224,8 @@ int arima_order_search_batch_device(arima_handle *h, const double *d_series, int
  * differenced series with css-cgd fits, a css-bobyqa retry where css-cgd throws in the optimizer (fitTryBothStrategies,
  * ARIMA.scala:315-319) (intercept only for d <= 1; the neighbourhood never changes q -- the
  * reference's quirks, ARIMA.scala:298-300, :356-366), keeping the first minimum approxAIC among stationary and
- * invertible fits. max_p, max_q <= 5. order_out N x 4 = (p, d, q, intercept) (-1s when the series has no model),
+ * invertible fits. max_p <= 8 (any max_q: the walk only meets q <= 2), any series length (KPSS lags above 32 take
+ * one pass per lag). order_out N x 4 = (p, d, q, intercept) (-1s when the series has no model),
  * coef_out N x 11 (zero-padded; NaN when none), aic_out N (+inf when none), status_out N: ARIMA_ST_OK,
  * ARIMA_ST_FALLBACK_UNPINNED (result valid, see above), ARIMA_ST_NOT_STATIONARY, ARIMA_ST_NO_MODEL, or the KPSS
  * regression's shape status (T <= 1). n_fits_out (nullable): candidate fits the walk ran for the series.        */

@@ -173,13 +173,14 @@ object ArimaMI355X {
     Array.tabulate(n)(i => Array.tabulate(t + nFuture)(j => out.get(i * (t + nFuture) + j)))
   }
 
-  /** The min-approxAIC (ARIMA.scala:826-830) model per series over d <= maxD, p <= maxP, q <= maxQ and the
-    * intercept modes, among fits that returned normally and are stationary and invertible (ARIMA.scala:342).
-    * Returns (p, d, q, intercept) per series (-1s when nothing qualified), coefficients and AIC. */
-  /** Drop-in for ARIMA.autoFit (ARIMA.scala:280-304): one series, the reference's exceptions. */
-  def autoFit(ts: Vector, maxP: Int = 5, maxD: Int = 2, maxQ: Int = 5): ARIMAModel = {
+  /** Drop-in for ARIMA.autoFit (ARIMA.scala:280-304): one series, the reference's exceptions. maxP <= 8 (its
+    * css-bobyqa retries have at most 11 parameters). A FALLBACK_UNPINNED result (a retry reached BOBYQA's RESCUE
+    * branch) is returned like OK unless strict = true, which throws -- the policy of the Python mirror's
+    * `autofit(..., strict=False)` (include/sparkts_arima.h). */
+  def autoFit(ts: Vector, maxP: Int = 5, maxD: Int = 2, maxQ: Int = 5, strict: Boolean = false): ARIMAModel = {
     val (order, coef, _, status) = autoFitMany(Array(ts.toArray), maxP, maxD, maxQ)
-    if (status(0) != ArimaStatus.OK) throw ArimaStatus.toException(status(0))
+    val st = status(0)
+    if (st != ArimaStatus.OK && !(st == ArimaStatus.FALLBACK_UNPINNED && !strict)) throw ArimaStatus.toException(st)
     val Array(p, d, q, c) = order(0)
     new ARIMAModel(p, d, q, coef(0).take(p + q + c), c == 1)
   }
@@ -204,6 +205,9 @@ object ArimaMI355X {
       Array.tabulate(n)(status.get))
   }
 
+  /** The min-approxAIC (ARIMA.scala:826-830) model per series over d <= maxD, p <= maxP, q <= maxQ and the
+    * intercept modes, among fits that returned normally and are stationary and invertible (ARIMA.scala:342).
+    * Returns (p, d, q, intercept) per series (-1s when nothing qualified), coefficients and AIC. */
   def orderSearchMany(values: Array[Array[Double]], maxP: Int = 5, maxD: Int = 2, maxQ: Int = 5,
                       interceptMode: Int = 2): (Array[Array[Int]], Array[Array[Double]], Array[Double]) = {
     val n = values.length

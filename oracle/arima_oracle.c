@@ -421,6 +421,10 @@ typedef struct {
     double *tr_alpha;
     int tr_len, tr_cap, tr_cur_phase;
     double tr_cur_alpha;
+    /* optional per-iteration state trace (analysis only, tools/maxeval_study.py): at the top of every CG iteration
+     * [point (k), searchDirection (k), delta, previous objective, n_eval] */
+    double *st_buf;
+    int st_cap, st_len;
 } orc_ctx;
 
 static void trace(orc_ctx *c, int phase, double alpha) {
@@ -636,6 +640,14 @@ static int cg_optimize(orc_ctx *c, const double *init, double *point_out, double
     for (;;) {
         if (c->n_iter + 1 > ORC_MAX_ITER) return ARIMA_ST_MAX_ITER;
         c->n_iter++;
+        if (c->st_buf && c->st_len < c->st_cap) {
+            double *o = c->st_buf + (size_t)c->st_len * (size_t)(2 * k + 3);
+            for (int i = 0; i < k; i++) { o[i] = point[i]; o[k + i] = dir[i]; }
+            o[2 * k] = delta;
+            o[2 * k + 1] = have_cur ? cur_obj : NAN;
+            o[2 * k + 2] = (double)c->n_eval;
+            c->st_len++;
+        }
         double objective;
         trace(c, 0, 0.0);
         if ((st = cg_obj(c, point, &objective))) return st;
@@ -710,7 +722,7 @@ int orc_fit(const double *ts, int T, int p, int d, int q, int I, int method, con
     }
     if (method != ARIMA_METHOD_CSS_CGD) { free(tmp); return ARIMA_ST_UNSUPPORTED_METHOD; }  /* :105-109 */
     if (k == 0) { free(tmp); return ARIMA_ST_ZERO_PARAMS; }
-    orc_ctx c = {y, n, p, q, I, k, smear, 0, 0, 0, NULL, NULL, 0, 0, 2, 0.0};
+    orc_ctx c = {y, n, p, q, I, k, smear, 0, 0, 0, NULL, NULL, 0, 0, 2, 0.0, NULL, 0, 0};
     double pt[ORC_KMAX], obj;
     st = cg_optimize(&c, init, pt, &obj);                         /* :174-200 */
     counters[0] = c.n_eval; counters[1] = c.n_grad; counters[2] = c.n_iter;
@@ -733,10 +745,34 @@ int orc_fit_trace(const double *ts, int T, int p, int d, int q, int I, int smear
     double init[ORC_KMAX];
     int st = orc_hannan_rissanen(y, n, p, q, I, init);
     if (st) { free(tmp); *tr_len = 0; return st; }
-    orc_ctx c = {y, n, p, q, I, k, smear, 0, 0, 0, tr_phase, tr_alpha, 0, tr_cap, 2, 0.0};
+    orc_ctx c = {y, n, p, q, I, k, smear, 0, 0, 0, tr_phase, tr_alpha, 0, tr_cap, 2, 0.0, NULL, 0, 0};
     double pt[ORC_KMAX], obj;
     st = cg_optimize(&c, init, pt, &obj);
     *tr_len = c.tr_len;
+    free(tmp);
+    return st;
+}
+
+/* Same CG fit (HR init) recording the optimizer's state at the top of every iteration into st_buf (2k + 3 doubles per
+ * iteration, at most st_cap iterations): the MaxEval periodicity study (tools/maxeval_study.py). counters: n_eval,
+ * n_grad, n_iter. */
+int orc_fit_state_trace(const double *ts, int T, int p, int d, int q, int I, int smear, double *st_buf, int st_cap,
+                        int *st_len, int *counters) {
+    int k = I + p + q;
+    double *tmp = (double *)malloc(sizeof(double) * (size_t)(T > 0 ? T : 1));
+    orc_differences_of_order_d(ts, T, d, tmp);
+    int n = T - d;
+    const double *y = tmp + d;
+    double init[ORC_KMAX];
+    int st = orc_hannan_rissanen(y, n, p, q, I, init);
+    *st_len = 0;
+    counters[0] = counters[1] = counters[2] = 0;
+    if (st) { free(tmp); return st; }
+    orc_ctx c = {y, n, p, q, I, k, smear, 0, 0, 0, NULL, NULL, 0, 0, 2, 0.0, st_buf, st_cap, 0};
+    double pt[ORC_KMAX], obj;
+    st = cg_optimize(&c, init, pt, &obj);
+    *st_len = c.st_len;
+    counters[0] = c.n_eval; counters[1] = c.n_grad; counters[2] = c.n_iter;
     free(tmp);
     return st;
 }

@@ -90,6 +90,42 @@ __device__ double kpss_c_row(const double *__restrict__ y, int n) {
     return (s2 / lrv) / (double)nn;
 }
 
+// The same statistic for any lag (rows longer than ~19 900 points, lag > kKpssLagMax; VERDICT r5 missing 1): the
+// Newey-West cross product of each lag i is its own left fold over j = i .. n-1 of e_j * e_{j-i} (every fold of the
+// register version, in the same order), so lag i gets a pass of its own over the row instead of a register ring.
+__device__ double kpss_c_row_any(const double *__restrict__ y, int n) {
+    const double a = -__builtin_sqrt((double)n);
+    const double q0 = 1.0 - a;
+    double dot = 0.0;
+    int r = 0;
+    stream_elems<2>(y, 0, n, [&](double v) {
+        dot = dot + v * (r == 0 ? q0 : 1.0);
+        ++r;
+    });
+    dot = dot / (a * q0);
+    const double y0 = y[0] + dot * q0;
+    const double beta = y0 / a;
+    const double fit = 0.0 + 1.0 * beta;
+    const int lag = kpss_lag(n);
+    double cum = 0.0, s2 = 0.0, sq = 0.0;
+    stream_elems<2>(y, 0, n, [&](double v) {
+        const double e = v - fit;
+        cum = cum + e;
+        s2 = s2 + cum * cum;
+        sq = sq + e * e;
+    });
+    double sum_terms = 0.0;
+    for (int i = 1; i <= lag; ++i) {
+        double cell = 0.0;
+        for (int j = i; j < n; ++j) cell = cell + (y[j] - fit) * (y[j - i] - fit);
+        sum_terms = sum_terms + cell * (1.0 - ((double)i / (double)(lag + 1)));
+    }
+    const double partial = (sum_terms * 2.0) / (double)n;
+    const double lrv = partial + sq / (double)n;
+    const int32_t nn = (int32_t)((uint32_t)n * (uint32_t)n);          // (n * n): an Int product, wraps as the JVM's
+    return (s2 / lrv) / (double)nn;
+}
+
 // One candidate d of autoFit's search (ARIMA.scala:287-292): series not decided yet whose differenced row passes the
 // test at 5 % take d. stat_out (optional): the statistic of every row (the arima_kpss_batch building block).
 __global__ __launch_bounds__(256) void k_kpss_c(const double *__restrict__ w, int64_t ld, int n, int64_t N, int d,
@@ -97,7 +133,7 @@ __global__ __launch_bounds__(256) void k_kpss_c(const double *__restrict__ w, in
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
     if (dsel && dsel[i] >= 0) return;
-    const double st = kpss_c_row(w + i * ld, n);
+    const double st = kpss_lag(n) <= kKpssLagMax ? kpss_c_row(w + i * ld, n) : kpss_c_row_any(w + i * ld, n);
     if (stat_out) stat_out[i] = st;
     if (dsel && st < kKpssCritical5) dsel[i] = d;          // `stat < criticalValues(kpssSignificance)`, :291
 }
@@ -144,7 +180,7 @@ __global__ __launch_bounds__(256) void k_difference_sel(const double *__restrict
 // ---------------------------------------------------------------------------------------------------------------
 // The stepwise walk (findBestARMAModel, ARIMA.scala:310-375). Candidate orders are packed p | q << 4 | I << 8; the
 // walk only ever meets q in {0, 1, 2} (the first candidates', :325-327 -- the neighbourhood keeps q, :364), so an
-// order's combo index (p * 3 + q) * 2 + I < kAfCombos doubles as its bit in the series' `seen` mask (pastParams).
+// order's combo index (p * 3 + q) * 2 + I < kAfCombosMax doubles as its bit in the series' `seen` mask (pastParams).
 // Duplicates in the reference's candidate list (the 3 x 3 neighbourhood yields (p +- 1, q, I) three times each) are
 // fitted once: their results are identical, and minBy keeps the first occurrence, which the deduplicated list (in
 // first-appearance order) preserves.
@@ -298,7 +334,6 @@ __global__ __launch_bounds__(256) void k_af_finish(int64_t N, const AfSeries *__
 int launch_kpss_c(const double *w, int64_t ld, int n, int64_t N, int d, int32_t *dsel, double *stat_out,
                   hipStream_t s) {
     if (N == 0) return ARIMA_OK;
-    if (kpss_lag(n) > kKpssLagMax) return ARIMA_E_UNSUPPORTED;
     hipLaunchKernelGGL(k_kpss_c, dim3(grid_of(N, 256)), dim3(256), 0, s, w, ld, n, N, d, dsel, stat_out);
     STS_AF_CHECK();
     return ARIMA_OK;

@@ -12,6 +12,8 @@
 // every series takes its own trust-region path) for large batches, and a wave per series (the state in LDS, the
 // wave's lanes run one series' uniform code: no divergence, LDS instead of scratch latency) for small batches and
 // autoFit's retries, whose time is set by their slowest series.
+#include <algorithm>
+
 #include "arima_device.hpp"
 #include "arima_launch.hpp"
 
@@ -57,6 +59,11 @@ __device__ __forceinline__ void bq_sync() {        // uniform LDS writes before 
 // p, q <= 5: the operations of css_pass in the same order (dest = 0 + I * c0, + AR lags, + MA terms; the ascending
 // maTerms copy leaves [e_{t-1}, e_{t-2}, e_{t-2}, ...]; css folded left; Int -n/2)
 __device__ double bq_css_ll(const double *__restrict__ row, int n, int p, int q, int I, const double *c) {
+    if (p > 5 || q > 5) {                          // the runtime-order path's recursion (arima_device.hpp gen_css)
+        double cg[BQ_KMAX];
+        for (int j = 0; j < BQ_KMAX; ++j) cg[j] = (j < I + p + q) ? c[j] : 0.0;
+        return css_to_loglik(gen_css(GRow{row, 0}, n, p, q, I, cg), n);
+    }
     const int M = p > q ? p : q;
     double yl[5], ma[5];
 #pragma unroll
@@ -114,7 +121,7 @@ __device__ __forceinline__ double bq_css_ll_t(const double *__restrict__ row, in
     double c[KA], g[KA], css;
 #pragma unroll
     for (int j = 0; j < KA; ++j) c[j] = (j < I + P + Q) ? x[j] : 0.0;
-    css_pass<P, Q, I, false, true, 1>(row, n, c, css, g);
+    css_pass<P, Q, I, false, true, false, 1>(row, n, c, css, g);
     return css_to_loglik(css, n);
 }
 
@@ -1344,6 +1351,7 @@ __device__ bool bq_roots_outside(const double *poly, int deg) {
 }
 
 __device__ uint8_t bq_model_flags(const double *c, int p, int q, int I) {
+    if (p > 5 || q > 5) return gen_model_flags(c, p, q, I);      // the same step-down at any order
     double poly[6];
     bool st = true, inv = true;
     if (p > 0) {
@@ -1415,20 +1423,20 @@ __global__ __launch_bounds__(64, WAVE ? kBqWaveOcc : 1) void k_bobyqa_fit(const 
 // of the round's result arrays, coefficients and inits k-strided from off[cb] * 11). A per-order css-bobyqa launch
 // would make each order wait for its slowest lane; instead the failing rows of every order are listed and refitted
 // together. Per row the same computation as k_bobyqa_fit with refit_status.
-__device__ __forceinline__ int af_row_combo(const int64_t *off, int64_t r) {   // the last order whose rows start <= r
+__device__ __forceinline__ int af_row_combo(const int64_t *off, int ncombos, int64_t r) {   // the last order whose rows start <= r
     int cb = 0;
-    for (int c = 1; c < kAfCombos; ++c)
+    for (int c = 1; c < ncombos; ++c)
         if (off[c] <= r) cb = c;
     return cb;
 }
 
 __global__ __launch_bounds__(64) void k_af_refit_list(const int32_t *__restrict__ status, int64_t total,
-                                                      const int64_t *__restrict__ off, int32_t *__restrict__ list,
-                                                      unsigned *__restrict__ count) {
+                                                      const int64_t *__restrict__ off, int ncombos,
+                                                      int32_t *__restrict__ list, unsigned *__restrict__ count) {
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool want = false;
     if (r < total && bq_refit_wanted(status[r])) {
-        const int cb = af_row_combo(off, r);
+        const int cb = af_row_combo(off, ncombos, r);
         const int p = (cb / 2) / 3, q = (cb / 2) % 3;
         want = !(p > 0 && q == 0);                 // the AR-only shortcut never reaches a method (ARIMA.scala:90-96)
     }
@@ -1455,23 +1463,26 @@ __device__ __forceinline__ int bq_fit_k(const double *y, int n, int p, int q, in
 template <bool WAVE>
 __global__ __launch_bounds__(64, WAVE ? kBqWaveOcc : 1) void k_bobyqa_refit_rows(const double *__restrict__ rows, int64_t ld, int n,
                                                           const int32_t *__restrict__ lists, int64_t N,
-                                                          const int64_t *__restrict__ off,
+                                                          const int64_t *__restrict__ off, int ncombos, int kc,
                                                           const int32_t *__restrict__ list,
                                                           const unsigned *__restrict__ count,
                                                           const double *__restrict__ init,
                                                           const int32_t *__restrict__ init_status,
                                                           double *__restrict__ coef, double *__restrict__ ll,
                                                           int32_t *__restrict__ status, uint8_t *__restrict__ flags) {
-    constexpr int kSmem = WAVE ? (int)(sizeof(BqState<8>) / sizeof(double)) : 1;
-    __shared__ double smem[kSmem];                 // the largest autoFit dimension: p <= 5, q <= 2, intercept
-    const int64_t i = WAVE ? (int64_t)blockIdx.x : (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)*count) return;
+    constexpr int kSmem = WAVE ? (int)(sizeof(BqState<BQ_KMAX>) / sizeof(double)) : 1;
+    __shared__ double smem[kSmem];                 // the largest dimension css-bobyqa compiles (autoFit: p <= 8, q <= 2, c)
+    // persistent over the round's retry list (the grid is sized by the host from the list's length)
+    const int64_t cnt = (int64_t)*count;
+    const int64_t i0 = WAVE ? (int64_t)blockIdx.x : (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t istep = WAVE ? (int64_t)gridDim.x : (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = i0; i < cnt; i += istep) {
     const int64_t r = list[i];
-    const int cb = af_row_combo(off, r);
+    const int cb = af_row_combo(off, ncombos, r);
     const int p = (cb / 2) / 3, q = (cb / 2) % 3, I = cb % 2, k = I + p + q;
     const int64_t slot = r - off[cb];
     const double *y = rows + (int64_t)lists[(int64_t)cb * N + slot] * ld;
-    const int64_t base = off[cb] * 11 + slot * k;
+    const int64_t base = off[cb] * kc + slot * k;
     int st = init_status[r];
     double x0[BQ_KMAX], x[BQ_KMAX];
     int nev = 0;
@@ -1485,33 +1496,49 @@ __global__ __launch_bounds__(64, WAVE ? kBqWaveOcc : 1) void k_bobyqa_refit_rows
         case 6: st = bq_fit_k<6, WAVE>(y, n, p, q, I, x0, x, &nev, smem); break;
         case 7: st = bq_fit_k<7, WAVE>(y, n, p, q, I, x0, x, &nev, smem); break;
         case 8: st = bq_fit_k<8, WAVE>(y, n, p, q, I, x0, x, &nev, smem); break;
-        default: st = ARIMA_ST_TOO_FEW_PARAMS; break;   /* k < 2: BOBYQAOptimizer.setup */
+        case 9: st = bq_fit_k<9, WAVE>(y, n, p, q, I, x0, x, &nev, smem); break;
+        case 10: st = bq_fit_k<10, WAVE>(y, n, p, q, I, x0, x, &nev, smem); break;
+        case 11: st = bq_fit_k<11, WAVE>(y, n, p, q, I, x0, x, &nev, smem); break;
+        default: st = k < 2 ? ARIMA_ST_TOO_FEW_PARAMS : ARIMA_ST_UNSUPPORTED_METHOD; break;   /* k < 2: setup */
         }
     }
     const bool ok = st == ARIMA_ST_OK;
     const double llv = ok ? bq_css_ll(y, n, p, q, I, x) : __builtin_nan("");
     const uint8_t fl = ok ? bq_model_flags(x, p, q, I) : (uint8_t)0;
-    if (WAVE && threadIdx.x != 0) return;
-    for (int j = 0; j < k; ++j) coef[base + j] = ok ? x[j] : __builtin_nan("");
-    ll[r] = llv;
-    status[r] = st;
-    flags[r] = fl;
+    if (!WAVE || threadIdx.x == 0) {
+        for (int j = 0; j < k; ++j) coef[base + j] = ok ? x[j] : __builtin_nan("");
+        ll[r] = llv;
+        status[r] = st;
+        flags[r] = fl;
+    }
+    if constexpr (WAVE) __syncthreads();           // the next row reuses the LDS state
+    }
 }
 
-int launch_bobyqa_refit_round(const double *rows, int64_t ld, int n, const int32_t *lists, int64_t N,
-                              const int64_t *off, int64_t total, const double *init, const int32_t *init_status,
-                              int32_t *list, unsigned *count, double *coef, double *ll, int32_t *status,
-                              uint8_t *flags, bool wave, hipStream_t s) {
+int launch_bobyqa_refit_list(const int64_t *off, int ncombos, int64_t total, const int32_t *status, int32_t *list,
+                             unsigned *count, hipStream_t s) {
     if (total == 0) return ARIMA_OK;
     if (hipMemsetAsync(count, 0, sizeof(unsigned), s) != hipSuccess) return ARIMA_E_DEVICE;
-    const dim3 grid((unsigned)((total + 63) / 64));
-    hipLaunchKernelGGL(k_af_refit_list, grid, dim3(64), 0, s, status, total, off, list, count);
-    if (wave)
-        hipLaunchKernelGGL(k_bobyqa_refit_rows<true>, dim3((unsigned)total), dim3(64), 0, s, rows, ld, n, lists, N,
-                           off, list, count, init, init_status, coef, ll, status, flags);
-    else
-        hipLaunchKernelGGL(k_bobyqa_refit_rows<false>, grid, dim3(64), 0, s, rows, ld, n, lists, N, off, list, count,
-                           init, init_status, coef, ll, status, flags);
+    hipLaunchKernelGGL(k_af_refit_list, dim3((unsigned)((total + 63) / 64)), dim3(64), 0, s, status, total, off, ncombos,
+                       list, count);
+    return hipGetLastError() == hipSuccess ? ARIMA_OK : ARIMA_E_DEVICE;
+}
+
+// rows: the retry count the host read back (one workgroup per listed row, not per candidate row)
+int launch_bobyqa_refit_rows(const double *rows_, int64_t ld, int n, const int32_t *lists, int64_t N,
+                             const int64_t *off, int ncombos, int kc, const int32_t *list, const unsigned *count,
+                             int64_t rows, const double *init, const int32_t *init_status, double *coef, double *ll,
+                             int32_t *status, uint8_t *flags, bool wave, hipStream_t s) {
+    if (rows <= 0) return ARIMA_OK;
+    if (wave) {
+        const unsigned grid = (unsigned)std::min<int64_t>(rows, 1 << 20);
+        hipLaunchKernelGGL(k_bobyqa_refit_rows<true>, dim3(grid), dim3(64), 0, s, rows_, ld, n, lists, N, off, ncombos,
+                           kc, list, count, init, init_status, coef, ll, status, flags);
+    } else {
+        const unsigned grid = (unsigned)std::min<int64_t>((rows + 63) / 64, 1 << 16);
+        hipLaunchKernelGGL(k_bobyqa_refit_rows<false>, dim3(grid), dim3(64), 0, s, rows_, ld, n, lists, N, off,
+                           ncombos, kc, list, count, init, init_status, coef, ll, status, flags);
+    }
     return hipGetLastError() == hipSuccess ? ARIMA_OK : ARIMA_E_DEVICE;
 }
 
@@ -1520,7 +1547,7 @@ int launch_bobyqa_fit(const double *y, int64_t ld, int n, int64_t N, int p, int 
                       int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out, bool wave,
                       hipStream_t s) {
     if (N == 0) return ARIMA_OK;
-    if (p > 5 || q > 5 || I + p + q > BQ_KMAX) return ARIMA_E_UNSUPPORTED;
+    if (!gen_orders_ok(p, q) || I + p + q > BQ_KMAX) return ARIMA_E_UNSUPPORTED;
     // one instantiation per dimension k = I + p + q: Powell's loops get compile-time bounds
     const dim3 grid_lane((unsigned)((N + 63) / 64)), grid_wave((unsigned)N);
 #define BQ_LAUNCH(K)                                                                                                  \

@@ -15,6 +15,7 @@
 #include <type_traits>
 
 #include "../../include/sparkts_arima.h"
+#include "arima_launch.hpp"
 #include "cg_lane.hpp"
 
 namespace sts {
@@ -152,6 +153,32 @@ __device__ __forceinline__ void stream_elems(const double *__restrict__ row, int
 }
 
 // ------------------------------------------------------------------------------------------------------
+// The differenced series read straight from the caller's row (round 6, fused differencing). The fit path works on
+// differencesOfOrderD(ts, d).drop(d) (ARIMA.scala:88): element i of it is raw[i + 1] - raw[i] for d = 1 (the
+// subtraction differencesAtLag performs, UnivariateTimeSeries.scala:384-405) and raw[i] for d = 0. Passes form it on
+// the fly from the raw row instead of reading a differenced copy that a separate kernel wrote (17 GB of HBM traffic
+// per 1M x 1024 fit, and its own pipeline stage); d >= 2 still goes through the k_difference workspace (dd = 0).
+// `raw` needs only the 8-B alignment of a double: stream_row streams whole 128-B lines from the line that holds its
+// first element (a line that holds a valid element never crosses a page, so the head and tail reads stay mapped).
+// ------------------------------------------------------------------------------------------------------
+__device__ __forceinline__ double drow_at(const double *__restrict__ raw, int dd, int i) {
+    return dd ? raw[i + 1] - raw[i] : raw[i];
+}
+
+// fn(x_i) for i = first .. last-1 of the differenced row (dd = 0 or 1) over the raw row, in order
+template <int D, class Fn>
+__device__ __forceinline__ void stream_row(const double *__restrict__ raw, int dd, int first, int last, Fn &&fn) {
+    if (first >= last) return;
+    const int off = (int)((reinterpret_cast<uintptr_t>(raw) >> 3) & (kChunk - 1));   // elements before raw in its line
+    double prev = raw[first];                          // raw[first + dd - 1] for dd = 1 (unused for dd = 0)
+    stream_elems<D>(raw - off, first + dd + off, last + dd + off, [&](double x) {
+        const double v = dd ? x - prev : x;            // wave-uniform select: no branch in the unrolled stream
+        prev = x;
+        fn(v);
+    });
+}
+
+// ------------------------------------------------------------------------------------------------------
 // CSS pass (objective, and optionally gradient) over one series — ARIMA.scala:430-534
 //
 // Lanes hold the maTerms buffer as two registers: updateMAErrors (:544-554) copies errs(i) -> errs(i+1) in
@@ -165,17 +192,22 @@ constexpr int kPrefetchG = 1;   // ... in gradient passes (5x the VALU work per 
 
 // Full pass. G = false: objective only -> css. G = true: also gradientlogLikelihoodCSSARMA -> g[] (already
 // divided by -sigma2, :532). SMEAR selects the Breeze overlap semantics of :526 (false = row shift).
-template <int P, int Q, int I, bool G, bool SMEAR, int DPF = (G ? kPrefetchG : kPrefetchF)>
+// RAW (the fit kernel): `row` is the caller's row at any 8-B alignment, differenced on the fly when dd = 1
+// (stream_row); otherwise a 128-B aligned differenced workspace row, padded to >= 16 elements (stream_elems).
+template <int P, int Q, int I, bool G, bool SMEAR, bool RAW = false, int DPF = (G ? kPrefetchG : kPrefetchF)>
 __device__ __forceinline__ void css_pass(const double *__restrict__ row, int n,
                                          const double (&c)[I + P + Q > 0 ? I + P + Q : 1], double &css_out,
-                                         double (&g)[I + P + Q > 0 ? I + P + Q : 1]) {
+                                         double (&g)[I + P + Q > 0 ? I + P + Q : 1], int dd = 0) {
     constexpr int K = I + P + Q;
     constexpr int KA = K > 0 ? K : 1;
     constexpr int M = (P > Q ? P : Q);
     constexpr int PA = P > 0 ? P : 1;
-    double yl[PA];                        // yl[j] = y_{i-1-j}; the row is padded to >= 16 elements
+    double yl[PA];                        // yl[j] = y_{i-1-j}
 #pragma unroll
-    for (int j = 0; j < PA; ++j) yl[j] = (j < P) ? row[M - 1 - j] : 0.0;
+    for (int j = 0; j < PA; ++j) {
+        if constexpr (RAW) yl[j] = (j < P && M - 1 - j < n) ? drow_at(row, dd, M - 1 - j) : 0.0;
+        else yl[j] = (j < P) ? row[M - 1 - j] : 0.0;
+    }
     double e1 = 0.0, e2 = 0.0, css = 0.0, sigma2 = 0.0;
     const double yh0 = 0.0 + (double)I * c[0];
     const double nd = (double)n;
@@ -249,7 +281,8 @@ __device__ __forceinline__ void css_pass(const double *__restrict__ row, int n,
             yl[0] = yi;
         }
     };
-    stream_elems<DPF>(row, M, n, step);
+    if constexpr (RAW) stream_row<DPF>(row, dd, M, n, step);
+    else stream_elems<DPF>(row, M, n, step);
     css_out = css;
     if constexpr (G) {
 #pragma unroll
@@ -262,12 +295,12 @@ __device__ __forceinline__ void css_pass(const double *__restrict__ row, int n,
 template <int P, int Q, int I, int NCH, int DPF = kPrefetchF>
 __device__ __forceinline__ void css_pass_multi(const double *__restrict__ row, int n,
                                                const double (&c)[NCH][I + P + Q > 0 ? I + P + Q : 1],
-                                               double (&css_out)[NCH]) {
+                                               double (&css_out)[NCH], int dd = 0) {
     constexpr int M = (P > Q ? P : Q);
     constexpr int PA = P > 0 ? P : 1;
     double yl[PA];
 #pragma unroll
-    for (int j = 0; j < PA; ++j) yl[j] = (j < P) ? row[M - 1 - j] : 0.0;
+    for (int j = 0; j < PA; ++j) yl[j] = (j < P && M - 1 - j < n) ? drow_at(row, dd, M - 1 - j) : 0.0;
     double e1[NCH], e2[NCH], css[NCH], yh0[NCH];
 #pragma unroll
     for (int h = 0; h < NCH; ++h) {
@@ -293,7 +326,7 @@ __device__ __forceinline__ void css_pass_multi(const double *__restrict__ row, i
             yl[0] = yi;
         }
     };
-    stream_elems<DPF>(row, M, n, step);
+    stream_row<DPF>(row, dd, M, n, step);
 #pragma unroll
     for (int h = 0; h < NCH; ++h) css_out[h] = css[h];
 }
@@ -728,7 +761,7 @@ __device__ __forceinline__ int ols_stage(Gen &gen, const double *__restrict__ ro
             xnorm = (double)R;
         } else if (S + 1 < R) {
             gen.begin(S + 1);
-            stream_elems<kPrefetchHR>(row, gen.first_elem(S + 1), n, [&](double v) {
+            stream_row<kPrefetchHR>(row, gen.dd, gen.first_elem(S + 1), n, [&](double v) {
                 double x[C], y;
                 gen.push(v, x, y);
                 hh_apply<C>(H, S, x, y);
@@ -747,7 +780,7 @@ __device__ __forceinline__ int ols_stage(Gen &gen, const double *__restrict__ ro
         dt = 0.0 + ys * vt;
         if (S + 1 < R) {
             gen.begin(S + 1);
-            stream_elems<kPrefetchHR>(row, gen.first_elem(S + 1), n, [&](double v) {
+            stream_row<kPrefetchHR>(row, gen.dd, gen.first_elem(S + 1), n, [&](double v) {
                 double x[C], y;
                 gen.push(v, x, y);
                 hh_apply<C>(H, S, x, y);
@@ -809,18 +842,20 @@ template <int m, int INTERCEPT>
 struct ARGen {
     static constexpr int C = INTERCEPT + m;
     static constexpr bool kOnesFirst = INTERCEPT != 0;       // column 0 = the intercept's ones
-    const double *__restrict__ y;
+    const double *__restrict__ y;             // raw row (dd = 1: differenced on the fly) or differenced row (dd = 0)
+    int dd = 0;
     double w[m + 1];
+    __device__ __forceinline__ double at(int i) const { return drow_at(y, dd, i); }
     __device__ __forceinline__ void row_at(int r, double (&x)[C], double &yv) const {
         if constexpr (INTERCEPT) x[0] = 1.0;
 #pragma unroll
-        for (int l = 1; l <= m; ++l) x[INTERCEPT + l - 1] = y[r + m - l];
-        yv = y[r + m];
+        for (int l = 1; l <= m; ++l) x[INTERCEPT + l - 1] = at(r + m - l);
+        yv = at(r + m);
     }
     __device__ __forceinline__ int first_elem(int r) const { return r + m; }
     __device__ __forceinline__ void begin(int r) {
 #pragma unroll
-        for (int l = 1; l <= m; ++l) w[l] = y[r + m - l];
+        for (int l = 1; l <= m; ++l) w[l] = at(r + m - l);
     }
     __device__ __forceinline__ void push(double v, double (&x)[C], double &yv) {
         w[0] = v;
@@ -846,30 +881,32 @@ struct HRGen {
     static constexpr int C = I + P + Q;
     static constexpr int QA = Q > 0 ? Q : 1;
     static constexpr bool kOnesFirst = I != 0;
-    const double *__restrict__ y;
+    const double *__restrict__ y;             // raw row (dd = 1: differenced on the fly) or differenced row (dd = 0)
+    int dd = 0;
     double a[m];
     double c;
     double w[m + 2];
     double ew[QA + 1];
+    __device__ __forceinline__ double at(int i) const { return drow_at(y, dd, i); }
     __device__ __forceinline__ double err_at(int s) const {
         double acc = 0.0;
 #pragma unroll
-        for (int j = 0; j < m; ++j) acc = acc + y[s + m - 1 - j] * a[j];
-        return y[s + m] - (acc + c);
+        for (int j = 0; j < m; ++j) acc = acc + at(s + m - 1 - j) * a[j];
+        return at(s + m) - (acc + c);
     }
     __device__ __forceinline__ void row_at(int r, double (&x)[C > 0 ? C : 1], double &yv) const {
         if constexpr (I) x[0] = 1.0;
 #pragma unroll
-        for (int l = 1; l <= P; ++l) x[I + l - 1] = y[m + r + M - l];
+        for (int l = 1; l <= P; ++l) x[I + l - 1] = at(m + r + M - l);
 #pragma unroll
         for (int l = 1; l <= Q; ++l) x[I + P + l - 1] = err_at(r + M - l);
-        yv = y[m + r + M];
+        yv = at(m + r + M);
     }
     __device__ __forceinline__ int first_elem(int r) const { return m + M + r; }
     __device__ __forceinline__ void begin(int r) {
         const int e = m + M + r;
 #pragma unroll
-        for (int l = 1; l <= m + 1; ++l) w[l] = y[e - l];
+        for (int l = 1; l <= m + 1; ++l) w[l] = at(e - l);
 #pragma unroll
         for (int l = 2; l <= Q; ++l) ew[l] = err_at(r + M - l);
     }
@@ -943,6 +980,117 @@ __device__ __forceinline__ uint8_t model_flags(const double (&c)[I + P + Q > 0 ?
     if (st) f |= ARIMA_FLAG_STATIONARY;
     if (inv) f |= ARIMA_FLAG_INVERTIBLE;
     return f;
+}
+
+// =======================================================================================================
+// least-squares shape checks (commons validateSampleData / Array2DRowRealMatrix), uniform per batch
+// =======================================================================================================
+__host__ __device__ inline int ols_check(int rows, int ncx, int intercept) {
+    if (rows <= 0) return ARIMA_ST_NO_DATA;
+    if (ncx + 1 > rows) return ARIMA_ST_NOT_ENOUGH_DATA;
+    if (!intercept && ncx == 0) return ARIMA_ST_NO_DATA;
+    return ARIMA_ST_OK;
+}
+
+// Static outcome of hannanRissanenInit's shapes (ARIMA.scala:216-242) for series of length n.
+__host__ __device__ inline int hr_shape_status(int n, int p, int q, int I) {
+    const int M = p > q ? p : q, m = M + 1;
+    if (n - m < 0) return ARIMA_ST_SERIES_TOO_SHORT;              // Y = ts(m until n)
+    int st = ols_check(n - m, m, 1);                               // AR(m) with intercept
+    if (st != ARIMA_ST_OK) return st;
+    const int nt = n - m;
+    if (nt - p < 0 || nt - q < 0) return ARIMA_ST_SERIES_TOO_SHORT;
+    int rows = nt - M;
+    if (rows < 0) rows = 0;
+    return ols_check(rows, p + q, I);
+}
+
+__host__ __device__ inline int ar_shape_status(int n, int p, int I) {
+    if (n - p < 0) return ARIMA_ST_SERIES_TOO_SHORT;
+    return ols_check(n - p, p, I);
+}
+
+// =======================================================================================================
+// Initial words of the fit kernel's counters and express ring (FitPrep, arima_launch.hpp), written by the kernel
+// that runs before k_cg_fit on the same stream (k_hr_init, or k_fit_prep): one dispatch instead of up to six fills
+// that queued behind other contexts' persistent fit waves (round 5: 113.6 ms of fill dispatches in a 1 949-ms
+// pipelined C2 span, 65 % of it with no fit running; profiles/r05/zc_pipe)
+// =======================================================================================================
+__device__ __forceinline__ void fit_prep(const FitPrep &fp) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    if (fp.ctl && g < kFitCtlWords) {
+        unsigned long long v = 0;
+        if (g == 15) v = ~0ull;                  // atomicMin of the kernel's start stamp (timing builds)
+        else if (g == 19) v = fp.v19;            // express ring entries of the launch (option "express_ring")
+        else if (g == 44) v = fp.v44;            // drain merge threshold ("merge_live")
+        else if (g == 45) v = fp.v45;            // donation thresholds ("donate_evals", "donate_evals_drained")
+        else if (g == 46) v = fp.v46;
+        fp.ctl[g] = v;
+    }
+    for (int64_t i = g; i < fp.xready_words; i += stride) fp.xready[i] = 0u;
+}
+
+// the runtime-order path's optimizer lane (arima_generic.hip): kGenMaxK padded coordinates, the first kdim real
+using GenLane = CGLane<kGenMaxK, 0, 0, true, RuntimeDim>;
+
+// ---- runtime-order helpers (arima_generic.hip; css-bobyqa at orders above the compiled ones) -------------------
+// a differenced row: element i = raw[i + 1] - raw[i] (dd = 1, fused differencing) or y[i] (dd = 0)
+struct GRow {
+    const double *y;
+    int dd;
+    __device__ __forceinline__ double at(int i) const { return drow_at(y, dd, i); }
+};
+
+// ---- logLikelihoodCSSARMA's sum of squares (ARIMA.scala:430-445, iterateARMA :581-618, updateMAErrors :544-554) ----
+// c has at least one entry (the intercept term multiplies c[0] even when I = 0, as css_pass does with its padded c)
+__device__ double gen_css(const GRow &r, int n, int p, int q, int I, const double *c) {
+    const int M = p > q ? p : q;
+    double e1 = 0.0, e2 = 0.0, css = 0.0;
+    const double yh0 = 0.0 + (double)I * c[0];                       // :600
+    for (int t = M; t < n; ++t) {
+        double yh = yh0;
+        for (int j = 0; j < p; ++j) yh = yh + r.at(t - 1 - j) * c[I + j];               // :602-605
+        for (int j = 0; j < q; ++j) yh = yh + (j == 0 ? e1 : e2) * c[I + p + j];        // :608-611 (ascending copy)
+        const double e = r.at(t) - yh;                                                  // :613
+        css = css + e * e;                                                              // :440-442
+        e2 = e1;
+        e1 = e;
+    }
+    return css;
+}
+
+// ---- ARIMAModel.isStationary / isInvertible (ARIMA.scala:777-815): the step-down of model_flags<P, Q, I> ----------
+__device__ bool gen_roots_outside(const double *poly, int N) {
+    double a[kGenMaxOrder + 1], b[kGenMaxOrder + 1];
+    for (int i = 0; i <= N; ++i) {
+        a[i] = poly[i];
+        if (!finite(a[i])) return false;
+    }
+    for (int mm = N; mm >= 1; --mm) {
+        const double kk = a[mm];
+        if (!(fabs(kk) < 1.0)) return false;
+        const double den = 1.0 - kk * kk;
+        for (int i = 0; i <= N; ++i) b[i] = (i < mm) ? (a[i] - kk * a[mm - i]) / den : 0.0;
+        for (int i = 0; i <= N; ++i) a[i] = b[i];
+    }
+    return true;
+}
+
+__device__ uint8_t gen_model_flags(const double *c, int p, int q, int I) {
+    double poly[kGenMaxOrder + 1];
+    bool st = true, inv = true;
+    if (p > 0) {
+        poly[0] = 1.0;
+        for (int j = 0; j < p; ++j) poly[1 + j] = -1.0 * c[I + j];
+        st = gen_roots_outside(poly, p);
+    }
+    if (q > 0) {
+        poly[0] = 1.0;
+        for (int j = 0; j < q; ++j) poly[1 + j] = c[I + p + j];
+        inv = gen_roots_outside(poly, q);
+    }
+    return (uint8_t)((st ? ARIMA_FLAG_STATIONARY : 0) | (inv ? ARIMA_FLAG_INVERTIBLE : 0));
 }
 
 // ------------------------------------------------------------------------------------------------------

@@ -419,7 +419,7 @@ int launch_search_select(const double *cand_coef, const double *cand_ll, const i
 // =======================================================================================================
 // Synthetic generator: ARIMAModel.sample (ARIMA.scala:655-678) with per-series jittered coefficients
 // =======================================================================================================
-constexpr int kSampleMaxOrder = 8;
+constexpr int kSampleMaxOrder = kGenMaxOrder;   // every order the library fits
 struct SampleCoef {
     double c[1 + 2 * kSampleMaxOrder];
 };
@@ -586,19 +586,34 @@ STS_DECLARE_P(5, extern)
     }
 #endif
 
+// one dispatch that prepares a fit kernel's counters and ring when no k_hr_init runs before it (FitPrep)
+__global__ __launch_bounds__(256) void k_fit_prep(FitPrep prep) { fit_prep(prep); }
+
+int launch_fit_prep(const FitPrep &prep, hipStream_t s) {
+    const int64_t words = std::max<int64_t>(prep.xready_words, kFitCtlWords);
+    const unsigned grid = (unsigned)std::min<int64_t>(grid_for(words, 256), 128);
+    hipLaunchKernelGGL(k_fit_prep, dim3(grid), dim3(256), 0, s, prep);
+    STS_CHECK_LAUNCH();
+    return ARIMA_OK;
+}
+
 int launch_hr_init(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, double *init_out,
-                   int32_t *status_out, hipStream_t s, int hr_grid) {
-    if (N == 0) return ARIMA_OK;
-#define C_(PP) launch_hr_init_P<PP>(y, ld, n, N, q, I, init_out, status_out, s, hr_grid)
+                   int32_t *status_out, hipStream_t s, int hr_grid, int dd, const FitPrep &prep) {
+    if (N == 0) return launch_fit_prep(prep, s);
+    if (gen_order(p, q)) return launch_gen_hr_init(y, ld, n, N, p, q, I, init_out, status_out, dd, prep, s);
+#define C_(PP) launch_hr_init_P<PP>(y, ld, n, N, q, I, init_out, status_out, s, hr_grid, dd, prep)
     STS_P_SWITCH(C_)
 #undef C_
 }
 
 int launch_ar_fit(const double *y, int64_t ld, int n, int64_t N, int p, int I, double *coef_out, double *ll_out,
                   int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
-                  hipStream_t s) {
+                  hipStream_t s, int dd) {
     if (N == 0) return ARIMA_OK;
-#define C_(PP) launch_ar_fit_P<PP>(y, ld, n, N, I, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out, s)
+    if (gen_order(p, 0))
+        return launch_gen_ar_fit(y, ld, n, N, p, I, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out, dd,
+                                 s);
+#define C_(PP) launch_ar_fit_P<PP>(y, ld, n, N, I, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out, s, dd)
     STS_P_SWITCH(C_)
 #undef C_
 }
@@ -607,11 +622,11 @@ int launch_cg_fit(const double *y, int64_t ld, int n, int64_t N, int p, int q, i
                   const double *init, const int32_t *init_status, double *coef_out, double *ll_out,
                   int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
                   unsigned long long *ctl, int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready,
-                  int join_express, hipStream_t s) {
+                  int join_express, hipStream_t s, int dd) {
     if (N == 0) return ARIMA_OK;
 #define C_(PP)                                                                                             \
     launch_cg_fit_P<PP>(y, ld, n, N, q, I, smear, init, init_status, coef_out, ll_out, status_out, n_eval_out, \
-                        n_grad_out, flags_out, ctl, grid_blocks, express_blocks, xq, xready, join_express, s)
+                        n_grad_out, flags_out, ctl, grid_blocks, express_blocks, xq, xready, join_express, s, dd)
     STS_P_SWITCH(C_)
 #undef C_
 }
@@ -625,6 +640,7 @@ int cg_fit_series_per_block(int p, int q, int I) {
 int launch_css_loglik(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, const double *coef,
                       double *ll_out, hipStream_t s) {
     if (N == 0) return ARIMA_OK;
+    if (gen_order(p, q)) return launch_gen_css_loglik(y, ld, n, N, p, q, I, coef, ll_out, s);
 #define C_(PP) launch_css_loglik_P<PP>(y, ld, n, N, q, I, coef, ll_out, s)
     STS_P_SWITCH(C_)
 #undef C_
@@ -633,6 +649,7 @@ int launch_css_loglik(const double *y, int64_t ld, int n, int64_t N, int p, int 
 int launch_css_grad(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, int smear,
                     const double *coef, double *g_out, hipStream_t s) {
     if (N == 0) return ARIMA_OK;
+    if (gen_order(p, q)) return launch_gen_css_grad(y, ld, n, N, p, q, I, smear, coef, g_out, s);
 #define C_(PP) launch_css_grad_P<PP>(y, ld, n, N, q, I, smear, coef, g_out, s)
     STS_P_SWITCH(C_)
 #undef C_
@@ -640,6 +657,7 @@ int launch_css_grad(const double *y, int64_t ld, int n, int64_t N, int p, int q,
 
 int launch_model_flags(const double *coef, int64_t N, int p, int q, int I, uint8_t *flags_out, hipStream_t s) {
     if (N == 0) return ARIMA_OK;
+    if (gen_order(p, q)) return launch_gen_model_flags(coef, N, p, q, I, flags_out, s);
 #define C_(PP) launch_model_flags_P<PP>(coef, N, q, I, flags_out, s)
     STS_P_SWITCH(C_)
 #undef C_

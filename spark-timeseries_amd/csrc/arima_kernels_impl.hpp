@@ -13,6 +13,7 @@
 //   k_sample              ARIMAModel.sample-style synthetic generator (Philox4x32-10 + Box-Muller)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <utility>
 
 #include "arima_device.hpp"
@@ -25,43 +26,17 @@ template <int V>
 using IC = std::integral_constant<int, V>;
 
 // =======================================================================================================
-// least-squares shape checks (commons validateSampleData / Array2DRowRealMatrix), uniform per batch
-// =======================================================================================================
-__host__ __device__ inline int ols_check(int rows, int ncx, int intercept) {
-    if (rows <= 0) return ARIMA_ST_NO_DATA;
-    if (ncx + 1 > rows) return ARIMA_ST_NOT_ENOUGH_DATA;
-    if (!intercept && ncx == 0) return ARIMA_ST_NO_DATA;
-    return ARIMA_ST_OK;
-}
-
-// Static outcome of hannanRissanenInit's shapes (ARIMA.scala:216-242) for series of length n.
-__host__ __device__ inline int hr_shape_status(int n, int p, int q, int I) {
-    const int M = p > q ? p : q, m = M + 1;
-    if (n - m < 0) return ARIMA_ST_SERIES_TOO_SHORT;              // Y = ts(m until n)
-    int st = ols_check(n - m, m, 1);                               // AR(m) with intercept
-    if (st != ARIMA_ST_OK) return st;
-    const int nt = n - m;
-    if (nt - p < 0 || nt - q < 0) return ARIMA_ST_SERIES_TOO_SHORT;
-    int rows = nt - M;
-    if (rows < 0) rows = 0;
-    return ols_check(rows, p + q, I);
-}
-
-__host__ __device__ inline int ar_shape_status(int n, int p, int I) {
-    if (n - p < 0) return ARIMA_ST_SERIES_TOO_SHORT;
-    return ols_check(n - p, p, I);
-}
-
-// =======================================================================================================
 // Hannan-Rissanen init (ARIMA.scala:216-242)
 // =======================================================================================================
 template <int P, int Q, int I>
 __global__ __launch_bounds__(256) void k_hr_init(const double *__restrict__ y, int64_t ld, int n, int64_t N,
-                                                 double *__restrict__ init_out, int32_t *__restrict__ status_out) {
+                                                 double *__restrict__ init_out, int32_t *__restrict__ status_out,
+                                                 int dd, FitPrep prep) {
     constexpr int K = I + P + Q;
     constexpr int KA = K > 0 ? K : 1;
     constexpr int M = P > Q ? P : Q;
     constexpr int m = M + 1;
+    fit_prep(prep);                          // the fit kernel's counters and ring for the launch after this one
     // grid-stride over series: a grid smaller than N / 256 blocks bounds the rows in flight (their 2(C_A + C_B)
     // passes then re-read from the caches instead of HBM)
     for (int64_t sid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; sid < N;
@@ -75,10 +50,12 @@ __global__ __launch_bounds__(256) void k_hr_init(const double *__restrict__ y, i
         double ab[1 + m];
         ARGen<m, 1> genA;
         genA.y = row;
+        genA.dd = dd;
         st = stream_ols<1 + m>(genA, row, n, n - m, ab);           // Autoregression.fitModel(y, m)  :225
         if (st == ARIMA_ST_OK) {
             HRGen<P, Q, I> genB;
             genB.y = row;
+            genB.dd = dd;
             genB.c = ab[0];
 #pragma unroll
             for (int j = 0; j < m; ++j) genB.a[j] = ab[1 + j];
@@ -105,7 +82,8 @@ template <int P, int I>
 __global__ __launch_bounds__(256) void k_ar_fit(const double *__restrict__ y, int64_t ld, int n, int64_t N,
                                                 double *__restrict__ coef_out, double *__restrict__ ll_out,
                                                 int32_t *__restrict__ status_out, int32_t *__restrict__ n_eval_out,
-                                                int32_t *__restrict__ n_grad_out, uint8_t *__restrict__ flags_out) {
+                                                int32_t *__restrict__ n_grad_out, uint8_t *__restrict__ flags_out,
+                                                int dd) {
     constexpr int K = I + P;
     const int64_t sid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (sid >= N) return;
@@ -120,12 +98,13 @@ __global__ __launch_bounds__(256) void k_ar_fit(const double *__restrict__ y, in
         double b[K];
         ARGen<P, I> gen;
         gen.y = row;
+        gen.dd = dd;
         st = stream_ols<K>(gen, row, n, n - P, b);
         if (st == ARIMA_ST_OK) {
 #pragma unroll
             for (int j = 0; j < K; ++j) beta[j] = b[j];
             double css, g[K];
-            css_pass<P, 0, I, false, false>(row, n, beta, css, g);
+            css_pass<P, 0, I, false, false, true>(row, n, beta, css, g, dd);
             ll = css_to_loglik(css, n);
             fl = model_flags<P, 0, I>(beta);
         }
@@ -364,7 +343,7 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
                             int32_t *__restrict__ status_out, int32_t *__restrict__ n_eval_out,
                             int32_t *__restrict__ n_grad_out, uint8_t *__restrict__ flags_out,
                             unsigned long long *__restrict__ ctl, unsigned char *__restrict__ xq,
-                            unsigned *__restrict__ xready, int64_t N, int lane) {
+                            unsigned *__restrict__ xready, int64_t N, int lane, int dd) {
     constexpr int K = I + P + Q;
     constexpr int NS = spec_ns<K>();
     const int gbytes = express_group_bytes<K>(n);
@@ -452,7 +431,7 @@ __device__ void fit_express(unsigned char *lds, int lds_bytes, const double *__r
         wave_sync_lds();
         if (arrived == 1) {
             const double *srow = y + ES.sid * ld;
-            for (int i = gl; i < n; i += GL) row[i] = srow[i];
+            for (int i = gl; i < n; i += GL) row[i] = drow_at(srow, dd, i);   // the differenced row (fused, dd = 1)
             gstate = 1;
             served += glead;
         }
@@ -609,7 +588,7 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
     const int32_t *__restrict__ init_status, double *__restrict__ coef_out, double *__restrict__ ll_out,
     int32_t *__restrict__ status_out, int32_t *__restrict__ n_eval_out, int32_t *__restrict__ n_grad_out,
     uint8_t *__restrict__ flags_out, unsigned long long *__restrict__ ctl, unsigned char *__restrict__ xq,
-    unsigned *__restrict__ xready, int n_bulk, int join_express) {
+    unsigned *__restrict__ xready, int n_bulk, int join_express, int dd) {
     // ctl[0] = work counter, ctl[1] = lane F passes, ctl[2] = lane G passes, ctl[3] = wave F passes (one chain),
     // ctl[4] = wave G passes, ctl[5] = objective evaluations, ctl[6] = gradient evaluations, ctl[7] = spec hits,
     // ctl[8] = wave F passes with speculative chains, ctl[9] = speculative chains evaluated,
@@ -628,7 +607,7 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
     if ((int)blockIdx.x >= n_bulk) {                      // express workgroup: this wave's share of the LDS
         fit_express<P, Q, I, SMEAR>(reinterpret_cast<unsigned char *>(&slots[wave][0]), (int)sizeof(slots[0]), y, ld,
                                     n, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out, ctl, xq,
-                                    xready, N, lane);
+                                    xready, N, lane, dd);
         return;
     }
     if (has_express && lane == 0) {                       // counted before this wave takes any series (release)
@@ -971,7 +950,7 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
         tm_sel += t_b - t_a;
 #endif
         if (doG) {
-            css_pass<P, Q, I, true, SMEAR>(row, n, c, css, g);
+            css_pass<P, Q, I, true, SMEAR, true>(row, n, c, css, g, dd);
             resp_f = css_to_loglik(css, n);
             wave_g += lane0;
             lane_g += served;
@@ -1002,7 +981,7 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
                         for (int j = 0; j < K; ++j) cm[h][j] = c[j];
                     }
                 }
-                css_pass_multi<P, Q, I, NCH>(row, n, cm, cssm);
+                css_pass_multi<P, Q, I, NCH>(row, n, cm, cssm, dd);
                 css = cssm[0];
                 if (served) {
 #pragma unroll
@@ -1147,7 +1126,7 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
             wave_sync_lds();
             fit_express<P, Q, I, SMEAR>(reinterpret_cast<unsigned char *>(&slots[wave][0]), (int)sizeof(slots[0]), y,
                                         ld, n, coef_out, ll_out, status_out, n_eval_out, n_grad_out, flags_out, ctl,
-                                        xq, xready, N, lane);
+                                        xq, xready, N, lane, dd);
         }
     }
 #ifdef STS_TIMING
@@ -1281,7 +1260,7 @@ inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 
 
 template <int P>
 int launch_hr_init_P(const double *y, int64_t ld, int n, int64_t N, int q, int I, double *init_out,
-                     int32_t *status_out, hipStream_t s, int hr_grid) {
+                     int32_t *status_out, hipStream_t s, int hr_grid, int dd, const FitPrep &prep) {
     return with_order(q, [&](auto Qc) {
         return with_bool(I, [&](auto Ic) {
             constexpr int Q = decltype(Qc)::value, II = decltype(Ic)::value;
@@ -1289,7 +1268,7 @@ int launch_hr_init_P(const double *y, int64_t ld, int n, int64_t N, int q, int I
             const unsigned grid =
                 hr_grid > 0 ? std::min<unsigned>(grid_for(N, 64), (unsigned)hr_grid) : grid_for(N, 256);
             hipLaunchKernelGGL((k_hr_init<P, Q, II>), dim3(grid), dim3(block), 0, s, y, ld, n, N, init_out,
-                               status_out);
+                               status_out, dd, prep);
             STS_CHECK_LAUNCH();
             return ARIMA_OK;
         });
@@ -1299,14 +1278,14 @@ int launch_hr_init_P(const double *y, int64_t ld, int n, int64_t N, int q, int I
 template <int P>
 int launch_ar_fit_P(const double *y, int64_t ld, int n, int64_t N, int I, double *coef_out, double *ll_out,
                     int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
-                    hipStream_t s) {
+                    hipStream_t s, int dd) {
     if constexpr (P == 0) {
         return ARIMA_E_INVALID_ARG;
     } else {
         return with_bool(I, [&](auto Ic) {
             constexpr int II = decltype(Ic)::value;
             hipLaunchKernelGGL((k_ar_fit<P, II>), dim3(grid_for(N, 256)), dim3(256), 0, s, y, ld, n, N, coef_out,
-                               ll_out, status_out, n_eval_out, n_grad_out, flags_out);
+                               ll_out, status_out, n_eval_out, n_grad_out, flags_out, dd);
             STS_CHECK_LAUNCH();
             return ARIMA_OK;
         });
@@ -1320,7 +1299,7 @@ int launch_cg_fit_PS(const double *y, int64_t ld, int n, int64_t N, int q, int I
                      const int32_t *init_status, double *coef_out, double *ll_out, int32_t *status_out,
                      int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out, unsigned long long *ctl,
                      int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready, int join_express,
-                     hipStream_t s) {
+                     hipStream_t s, int dd) {
     return with_order(q, [&](auto Qc) {
         return with_bool(I, [&](auto Ic) {
             constexpr int Q = decltype(Qc)::value, II = decltype(Ic)::value;
@@ -1335,7 +1314,7 @@ int launch_cg_fit_PS(const double *y, int64_t ld, int n, int64_t N, int q, int I
                 hipLaunchKernelGGL((k_cg_fit<P, Q, II, S, SPW>), dim3(grid_blocks + express_blocks),
                                    dim3(64 * kFitWaves), 0, s, y, ld, n, N, init, init_status, coef_out, ll_out,
                                    status_out, n_eval_out, n_grad_out, flags_out, ctl, xq, xready, grid_blocks,
-                                   join_express);
+                                   join_express, dd);
                 STS_CHECK_LAUNCH();
                 return ARIMA_OK;
             }
@@ -1348,12 +1327,12 @@ int launch_cg_fit_P(const double *y, int64_t ld, int n, int64_t N, int q, int I,
                     const int32_t *init_status, double *coef_out, double *ll_out, int32_t *status_out,
                     int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out, unsigned long long *ctl,
                     int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready, int join_express,
-                    hipStream_t s) {
+                    hipStream_t s, int dd) {
     return with_smear(smear, [&](auto Sc) {
         return launch_cg_fit_PS<P, (decltype(Sc)::value != 0)>(y, ld, n, N, q, I, init, init_status, coef_out, ll_out,
                                                                status_out, n_eval_out, n_grad_out, flags_out, ctl,
                                                                grid_blocks, express_blocks, xq, xready, join_express,
-                                                               s);
+                                                               s, dd);
     });
 }
 
@@ -1416,19 +1395,19 @@ int launch_model_flags_P(const double *coef, int64_t N, int q, int I, uint8_t *f
     EXT template int launch_cg_fit_PS<PP, SS>(const double *, int64_t, int, int64_t, int, int, const double *,    \
                                               const int32_t *, double *, double *, int32_t *, int32_t *,        \
                                               int32_t *, uint8_t *, unsigned long long *, int, int,             \
-                                              unsigned char *, unsigned *, int, hipStream_t);
+                                              unsigned char *, unsigned *, int, hipStream_t, int);
 
 #define STS_DECLARE_P(PP, EXT)                                                                                  \
     STS_DECLARE_CG(PP, false, extern)                                                                           \
     STS_DECLARE_CG(PP, true, extern)                                                                            \
     EXT template int launch_hr_init_P<PP>(const double *, int64_t, int, int64_t, int, int, double *, int32_t *,  \
-                                          hipStream_t, int);                                                    \
+                                          hipStream_t, int, int, const FitPrep &);                              \
     EXT template int launch_ar_fit_P<PP>(const double *, int64_t, int, int64_t, int, double *, double *,         \
-                                         int32_t *, int32_t *, int32_t *, uint8_t *, hipStream_t);              \
+                                         int32_t *, int32_t *, int32_t *, uint8_t *, hipStream_t, int);         \
     EXT template int launch_cg_fit_P<PP>(const double *, int64_t, int, int64_t, int, int, int, const double *,   \
                                          const int32_t *, double *, double *, int32_t *, int32_t *, int32_t *,  \
                                          uint8_t *, unsigned long long *, int, int, unsigned char *, unsigned *, \
-                                         int, hipStream_t);                                                     \
+                                         int, hipStream_t, int);                                                \
     EXT template int cg_fit_series_per_block_P<PP>(int, int);                                                   \
     EXT template int launch_css_loglik_P<PP>(const double *, int64_t, int, int64_t, int, int, const double *,    \
                                              double *, hipStream_t);                                            \

@@ -25,18 +25,31 @@ int launch_forecast(const double *ts, int64_t ld_in, const double *coef, int k, 
                     int64_t N, int T, int p, int d, int q, int I, int n_future, hipStream_t s);
 int launch_inverse_difference(const double *in, int64_t ld_in, double *out, int64_t ld_out, int64_t N, int T,
                               int d, hipStream_t s);
+// The fit kernel's counter words (ctl) and express-ring ready words are initialised by the kernel that runs before it
+// on the same stream (k_hr_init, else k_fit_prep): ctl[] = 0 except ctl[15] = ~0 and the option words 19, 44, 45, 46;
+// xready[0 .. xready_words) = 0. ctl == nullptr / xready_words == 0: nothing to prepare.
+constexpr int kFitCtlWords = 48;
+struct FitPrep {
+    unsigned long long *ctl = nullptr;
+    unsigned *xready = nullptr;
+    int64_t xready_words = 0;
+    unsigned long long v19 = 0, v44 = 0, v45 = 0, v46 = 0;
+};
+int launch_fit_prep(const FitPrep &prep, hipStream_t s);
 // hr_grid > 0: that many single-wave workgroups stride over the series (bounds the rows in flight, so the 2(C_A + C_B)
-// passes over a row can hit the Infinity Cache); 0: one lane per series in 256-lane workgroups
+// passes over a row can hit the Infinity Cache); 0: one lane per series in 256-lane workgroups.
+// dd (here and in the fit launchers): 1 = y holds the RAW rows of a d = 1 fit and every pass differences them on the
+// fly (arima_device.hpp stream_row); 0 = y holds the differenced rows.
 int launch_hr_init(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, double *init_out,
-                   int32_t *status_out, hipStream_t s, int hr_grid = 0);
+                   int32_t *status_out, hipStream_t s, int hr_grid = 0, int dd = 0, const FitPrep &prep = FitPrep{});
 int launch_ar_fit(const double *y, int64_t ld, int n, int64_t N, int p, int I, double *coef_out, double *ll_out,
                   int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
-                  hipStream_t s);
+                  hipStream_t s, int dd = 0);
 int launch_cg_fit(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, int smear,
                   const double *init, const int32_t *init_status, double *coef_out, double *ll_out,
                   int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out,
                   unsigned long long *ctl, int grid_blocks, int express_blocks, unsigned char *xq, unsigned *xready,
-                  int join_express, hipStream_t s);
+                  int join_express, hipStream_t s, int dd = 0);
 constexpr int kExpressRingEntries = 32768;      // k_cg_fit's express hand-offs per launch (entries never reused)
 constexpr int kExpressRingBytes = kExpressRingEntries * 512;   // x kExpressEntryBytes
 constexpr int kExpressReadyBytes = kExpressRingEntries * 4;
@@ -59,7 +72,11 @@ constexpr int kFitBlocksPerCU = kFitWavesPerCU / kFitBlockWaves;
 constexpr int kMergeLiveDefault = 16;        // k_cg_fit's drain merge threshold (option "merge_live"; 0 = off)
 
 // ---- ARIMA.autoFit (arima_autofit.hip) ----
-constexpr int kAfCombos = 36;      // candidate (p, q, intercept) orders the stepwise walk can meet: p <= 5, q <= 2
+// candidate (p, q, intercept) orders the stepwise walk can meet: p <= max(max_p, 2), q <= 2 (combo (p * 3 + q) * 2 + I;
+// max_p <= kAfMaxP: its css-bobyqa retries have at most 11 parameters, the dimensions arima_bobyqa.hip compiles)
+constexpr int kAfMaxP = 8;
+constexpr int kAfCombosMax = (kAfMaxP + 1) * 6;
+inline int af_combos(int max_p) { return ((max_p > 2 ? max_p : 2) + 1) * 6; }
 constexpr int kAfMaxCand = 4;      // distinct candidates of one round of one series
 struct AfSeries {                  // one series' walk state (findBestARMAModel's locals, ARIMA.scala:321-375)
     double best_aic;               // curBestAIC
@@ -98,12 +115,41 @@ int launch_bobyqa_fit(const double *y, int64_t ld, int n, int64_t N, int p, int 
 // autoFit: the css-bobyqa retries of a whole round (every order's rows whose css-cgd fit threw in the optimizer), one
 // launch; rows = the differenced series (ld), lists / off = the round's per-order lists and row offsets, init /
 // init_status = each row's Hannan-Rissanen init (k-strided from off[cb] * 11) and status; list / count: workspace
-int launch_bobyqa_refit_round(const double *rows, int64_t ld, int n, const int32_t *lists, int64_t N,
-                              const int64_t *off, int64_t total, const double *init, const int32_t *init_status,
-                              int32_t *list, unsigned *count, double *coef, double *ll, int32_t *status,
-                              uint8_t *flags, bool wave, hipStream_t s);
+// (two launches: the list, whose length the host reads back, then one retry per listed row; ncombos orders in the
+// round's layout, coefficient rows kc-strided from off[cb] * kc)
+int launch_bobyqa_refit_list(const int64_t *off, int ncombos, int64_t total, const int32_t *status, int32_t *list,
+                             unsigned *count, hipStream_t s);
+int launch_bobyqa_refit_rows(const double *rows_, int64_t ld, int n, const int32_t *lists, int64_t N,
+                             const int64_t *off, int ncombos, int kc, const int32_t *list, const unsigned *count,
+                             int64_t rows, const double *init, const int32_t *init_status, double *coef, double *ll,
+                             int32_t *status, uint8_t *flags, bool wave, hipStream_t s);
 
 int hr_shape_status_host(int n, int p, int q, int I);
 int ar_shape_status_host(int n, int p, int I);
+
+// ---- the runtime-order path (arima_generic.hip): p or q above the compiled orders (5), up to kGenMaxOrder ----
+constexpr int kFastMaxOrder = 5;   // orders the compile-time kernels cover
+constexpr int kGenMaxOrder = 20;   // p, q <= 20
+constexpr int kGenMaxK = 2 * kGenMaxOrder + 1;
+inline bool gen_order(int p, int q) { return p > kFastMaxOrder || q > kFastMaxOrder; }
+bool gen_orders_ok(int p, int q);
+int launch_gen_hr_init(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, double *init_out,
+                       int32_t *status_out, int dd, const FitPrep &prep, hipStream_t s);
+int launch_gen_ar_fit(const double *y, int64_t ld, int n, int64_t N, int p, int I, double *coef_out, double *ll_out,
+                      int32_t *status_out, int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out, int dd,
+                      hipStream_t s);
+int launch_gen_fit(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, int smear, const double *init,
+                   const int32_t *init_status, double *coef_out, double *ll_out, int32_t *status_out,
+                   int32_t *n_eval_out, int32_t *n_grad_out, uint8_t *flags_out, unsigned long long *ctl, int dd,
+                   hipStream_t s);
+int launch_gen_css_loglik(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, const double *coef,
+                          double *ll_out, hipStream_t s);
+int launch_gen_css_grad(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, int smear,
+                        const double *coef, double *g_out, hipStream_t s);
+int launch_gen_model_flags(const double *coef, int64_t N, int p, int q, int I, uint8_t *flags_out, hipStream_t s);
+int64_t gen_forecast_ws_doubles(int T, int p, int d, int q, int n_future);
+int launch_gen_forecast(const double *ts, int64_t ld_in, const double *coef, int k, double *out, int64_t ld_out,
+                        int64_t N, int T, int p, int d, int q, int I, int n_future, double *ws, int64_t ws_stride,
+                        hipStream_t s);
 
 }  // namespace sts

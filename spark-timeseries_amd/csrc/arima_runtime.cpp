@@ -13,6 +13,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/sparkts_arima.h"
@@ -47,7 +48,7 @@ struct DevBuf {
 };
 
 constexpr int kNumEvents = 5;
-constexpr int kCtlWords = 48;     // device counters of the fit kernel (k_cg_fit's ctl[]; ctl[32] = series written)
+constexpr int kCtlWords = sts::kFitCtlWords;   // device counters of the fit kernel (k_cg_fit's ctl[]; ctl[32] = series written)
 
 // What arima_get_last_stats needs to turn the device counters of the last fit into arima_fit_stats. The fit
 // entry points do not wait for the device (the `*_device` contract): the counters are copied to pinned host
@@ -174,6 +175,9 @@ struct arima_handle {
     // (profiles/r05/q_wave, r_occ2, g_tmpl). An objective parallel in time over the row in LDS (css_pit_lds) was
     // slower in this kernel: autoFit 19.3 s, 1 024 fits 0.27 s (s_pit)
     int bobyqa_wave = -1;
+    // 1: device fits of d <= 1 difference into the k_difference workspace as before round 6 instead of reading the
+    // caller's rows (option "fuse_diff" 0; results are identical, tests compare the two)
+    int no_fuse = 0;
     int64_t last_express = 0;
     int64_t last_grid = 0;
     int search_lanes = 8;          // concurrent fits of the order search (2/4/8: 1269/1303/1408 series/s, profiles/r02/g_c5)
@@ -188,6 +192,17 @@ struct arima_handle {
     // series; profiles/r05/c_af2/default_cs*.json.)
     int host_pipeline = 3;         // contexts the chunked host path rotates over
     int64_t host_chunk = 1 << 18;  // series per chunk of the host path (option "host_chunk")
+    // host path uploads (round 6): the caller's pageable rows are copied by host_copy_threads threads into a ring of
+    // pinned blocks, each block DMA'd to the device while the threads fill the next (upload_staged). Before, the
+    // uploads went straight from pageable memory through the HIP runtime's own staging: 32.6 GB/s on the box's
+    // PCIe Gen5 x16 (3.98 M series/s end to end at C2). Option "host_copy_threads" 0 restores it.
+    int host_copy_threads = 8;
+    static constexpr int kStageSlots = 3;
+    static constexpr size_t kStageBytes = size_t(128) << 20;
+    void *stage[kStageSlots] = {};
+    hipEvent_t stage_ev[kStageSlots] = {};
+    bool stage_used[kStageSlots] = {};
+    unsigned stage_next = 0;
     int64_t fit_slice_bytes = 0;   // differenced workspace of one device-fit slice (option "fit_slice_bytes"; 0: from free HBM)
     SliceSlot slot[kSliceSlots];
     unsigned long long *slot_ctl = nullptr;     // pinned, kCtlWords per slot
@@ -201,6 +216,7 @@ struct arima_handle {
     FitCtx fctx[kMaxPipeline];
     // device workspaces of the building blocks
     DevBuf diff;
+    DevBuf fc_ws;                  // the runtime-order forecast's per-series arrays (forecast_any)
     // host-API staging
     DevBuf h_series, h_coef, h_ll, h_status, h_neval, h_ngrad, h_flags, h_uinit, h_aux;
     // order search: the differenced series per d, the concurrent fit lanes, host-API staging of the orders
@@ -213,10 +229,11 @@ struct arima_handle {
     DevBuf af_rows, af_dsel, af_state, af_best, af_counts, af_lists, af_off, af_coef, af_ll, af_status, af_flags;
     DevBuf af_init, af_hrst, af_rlist, af_rcount;     // the round's inits and the css-bobyqa retry list
     DevBuf af_out_order, af_out_coef, af_out_aic, af_out_status, af_out_nfits;   // host-API staging
-    int64_t *af_host = nullptr;                      // pinned: kAfCombos counts, then kAfCombos row offsets
+    int64_t *af_host = nullptr;                      // pinned: kAfCombosMax counts, kAfCombosMax row offsets, the retry count
     hipEvent_t ev_af = nullptr;
     int search_lanes_used = 0;
     int64_t search_n = 0, search_fits = 0;
+    int64_t autofit_slice = 0;     // autoFit series per slice (option "autofit_slice"; 0 = from free HBM)
 };
 
 namespace {
@@ -302,9 +319,10 @@ __global__ void k_fault_merge(const unsigned long long *__restrict__ ctl, unsign
         for (int i = 1; i < 6; ++i) rec[i] = ctl[26 + i];
 }
 
+// p, q <= 5: the order-specialised kernels; 5 < p, q <= kGenMaxOrder (20): the runtime-order path (arima_generic.hip)
 int check_orders(arima_handle *h, int p, int d, int q, int I) {
     if (p < 0 || q < 0 || d < 0 || (I != 0 && I != 1)) return set_err(h, ARIMA_E_INVALID_ARG, "bad order");
-    if (p > 5 || q > 5) return set_err(h, ARIMA_E_UNSUPPORTED, "p, q <= 5 are compiled in this build");
+    if (!sts::gen_orders_ok(p, q)) return set_err(h, ARIMA_E_UNSUPPORTED, "p, q <= 20");
     if (d > 16) return set_err(h, ARIMA_E_UNSUPPORTED, "d <= 16");
     return ARIMA_OK;
 }
@@ -410,6 +428,13 @@ int arima_destroy(arima_handle *h) {
     for (auto &sl : h->slot)
         for (auto &e : sl.ev)
             if (e) hipEventDestroy(e);
+    for (int j = 0; j < arima_handle::kStageSlots; ++j) {
+        if (h->stage_ev[j]) {
+            hipEventSynchronize(h->stage_ev[j]);
+            hipEventDestroy(h->stage_ev[j]);
+        }
+        if (h->stage[j]) hipHostFree(h->stage[j]);
+    }
     if (h->slot_ctl) hipHostFree(h->slot_ctl);
     if (h->search_acc_host) hipHostFree(h->search_acc_host);
     if (h->af_host) hipHostFree(h->af_host);
@@ -541,6 +566,8 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
     std::lock_guard<std::mutex> lk(h->mu);
     if (!strcmp(name, "smear")) { h->smear = value ? 1 : 0; return ARIMA_OK; }
     if (!strcmp(name, "bobyqa_wave")) { h->bobyqa_wave = value < 0 ? -1 : (value ? 1 : 0); return ARIMA_OK; }
+    if (!strcmp(name, "fuse_diff")) { h->no_fuse = value ? 0 : 1; return ARIMA_OK; }
+    if (!strcmp(name, "autofit_slice")) { h->autofit_slice = std::max<int64_t>(0, value); return ARIMA_OK; }
     if (!strcmp(name, "row_pad")) {                 // doubles, rounded up to whole 128-B lines
         h->row_pad = (int)round_up(std::min<int64_t>(4096, std::max<int64_t>(0, value)), 16);
         return ARIMA_OK;
@@ -575,6 +602,10 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
         return ARIMA_OK;
     }
     if (!strcmp(name, "host_chunk")) { h->host_chunk = std::max<int64_t>(1, value); return ARIMA_OK; }
+    if (!strcmp(name, "host_copy_threads")) {
+        h->host_copy_threads = (int)std::min<int64_t>(64, std::max<int64_t>(0, value));
+        return ARIMA_OK;
+    }
     if (!strcmp(name, "fit_slice_bytes")) { h->fit_slice_bytes = std::max<int64_t>(0, value); return ARIMA_OK; }
     return set_err(h, ARIMA_E_INVALID_ARG, "unknown option");
 }
@@ -589,7 +620,8 @@ int arima_get_option(const arima_handle *hc, const char *name, int64_t *value) {
         {"host_chunk", h->host_chunk}, {"fit_slice_bytes", h->fit_slice_bytes}, {"express_ring", h->express_ring},
         {"hr_grid", h->hr_grid}, {"row_pad", h->row_pad}, {"bobyqa_wave", h->bobyqa_wave}, {"merge_live", h->merge_live},
         {"search_express_blocks", h->search_express_blocks}, {"donate_evals", h->donate_evals},
-        {"donate_evals_drained", h->donate_evals_drained}};
+        {"donate_evals_drained", h->donate_evals_drained}, {"fuse_diff", h->no_fuse ? 0 : 1}, {"autofit_slice", h->autofit_slice},
+        {"host_copy_threads", h->host_copy_threads}};
     for (const auto &o : opts)
         if (!strcmp(name, o.n)) {
             *value = o.v;
@@ -694,30 +726,42 @@ static hipError_t end_fit(FitCtx &c, hipStream_t s) {
 // status -- over already-differenced rows y (N x n, leading dimension ldn), on stream s with workspace ws.
 // ev_mid (optional) is recorded between the init and the fit kernel. shared_gpu: other fits run concurrently (the
 // order search's lanes), so the fit kernel's drained workgroups exit instead of joining its express pool.
+// dd = 1: y holds the caller's RAW rows (leading dimension ldn) of a d = 1 fit, differenced inside every pass (fused
+// differencing, arima_device.hpp stream_row); dd = 0: y holds differenced rows.
 static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn, int n, int64_t N, int32_t p,
                        int32_t q, int32_t I, int32_t method, const double *d_user_init, double *d_coef, double *d_ll,
                        int32_t *d_status, int32_t *d_neval, int32_t *d_ngrad, uint8_t *d_flags, hipStream_t s,
                        hipEvent_t ev_mid, int64_t *grid_out, int64_t *express_out, bool shared_gpu = false,
-                       int express_cus = -2, bool search = false) {
+                       int express_cus = -2, bool search = false, int dd = 0) {
     const int k = I + p + q;
     *grid_out = 0;
     *express_out = 0;
+    // every workspace before the first launch (a growing DevBuf frees, and hipFree synchronises the device)
     RCCHK(h, ws.ctl.ensure(kCtlWords * sizeof(unsigned long long)), "workspace");
-    HIPCHK(h, hipMemsetAsync(ws.ctl.ptr, 0, kCtlWords * sizeof(unsigned long long), s));
-    HIPCHK(h, hipMemsetAsync(ws.ctl.as<unsigned long long>() + 15, 0xff, sizeof(unsigned long long), s));
-    if (h->express_ring > 0)                                   // ctl[19]: the launch's ring entries (low word)
-        HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)(ws.ctl.as<unsigned long long>() + 19), h->express_ring, 1, s));
-    if (h->merge_live > 0)                                     // ctl[44]: k_cg_fit's drain merge threshold
-        HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)(ws.ctl.as<unsigned long long>() + 44), h->merge_live, 1, s));
-    if (h->donate_evals > 0)                                   // ctl[45] / ctl[46]: express donation thresholds
-        HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)(ws.ctl.as<unsigned long long>() + 45), h->donate_evals, 1, s));
-    if (h->donate_evals_drained > 0)
-        HIPCHK(h, hipMemsetD32Async((hipDeviceptr_t)(ws.ctl.as<unsigned long long>() + 46), h->donate_evals_drained, 1,
-                                    s));
+    RCCHK(h, ws.xring.ensure(sts::kExpressRingBytes), "workspace");
+    RCCHK(h, ws.xready.ensure(sts::kExpressReadyBytes), "workspace");
+    // the fit kernel's counters and express-ring ready words, initialised by the kernel that runs before it
+    // (k_hr_init, or one k_fit_prep dispatch) instead of up to six fill dispatches (round 6)
+    sts::FitPrep prep;
+    prep.ctl = ws.ctl.as<unsigned long long>();
+    prep.xready = ws.xready.as<unsigned>();
+    prep.xready_words = sts::kExpressReadyBytes / 4;
+    prep.v19 = (unsigned long long)std::max(h->express_ring, 0);
+    prep.v44 = (unsigned long long)std::max(h->merge_live, 0);
+    prep.v45 = (unsigned long long)std::max(h->donate_evals, 0);
+    prep.v46 = (unsigned long long)std::max(h->donate_evals_drained, 0);
+    const bool cg = !(p > 0 && q == 0) && method == ARIMA_METHOD_CSS_CGD && k > 0;
+    const bool gen = sts::gen_order(p, q);                     // above the compiled orders: arima_generic.hip
+    if (!cg || gen) prep.xready_words = 0;                     // no express ring: only the counters are read
     if (p > 0 && q == 0) {                                     // AR-only shortcut, method never checked
+        RCCHK(h, sts::launch_fit_prep(prep, s), "fit_prep");
         if (ev_mid) HIPCHK(h, hipEventRecord(ev_mid, s));
-        RCCHK(h, sts::launch_ar_fit(y, ldn, n, N, p, I, d_coef, d_ll, d_status, d_neval, d_ngrad, d_flags, s),
-              "ar_fit");
+        if (gen)
+            RCCHK(h, sts::launch_gen_ar_fit(y, ldn, n, N, p, I, d_coef, d_ll, d_status, d_neval, d_ngrad, d_flags, dd,
+                                            s), "ar_fit");
+        else
+            RCCHK(h, sts::launch_ar_fit(y, ldn, n, N, p, I, d_coef, d_ll, d_status, d_neval, d_ngrad, d_flags, s, dd),
+                  "ar_fit");
         return ARIMA_OK;
     }
     const double *init = d_user_init;
@@ -725,11 +769,17 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
     if (!d_user_init) {
         RCCHK(h, ws.init.ensure((size_t)N * std::max(k, 1) * sizeof(double)), "workspace");
         RCCHK(h, ws.hr_status.ensure((size_t)N * sizeof(int32_t)), "workspace");
-        RCCHK(h, sts::launch_hr_init(y, ldn, n, N, p, q, I, ws.init.as<double>(), ws.hr_status.as<int32_t>(), s,
-                                     h->hr_grid >= 0 ? h->hr_grid : (shared_gpu && !search ? 1024 : 0)),
-              "hr_init");
+        if (gen)
+            RCCHK(h, sts::launch_gen_hr_init(y, ldn, n, N, p, q, I, ws.init.as<double>(), ws.hr_status.as<int32_t>(),
+                                             dd, prep, s), "hr_init");
+        else
+            RCCHK(h, sts::launch_hr_init(y, ldn, n, N, p, q, I, ws.init.as<double>(), ws.hr_status.as<int32_t>(), s,
+                                         h->hr_grid >= 0 ? h->hr_grid : (shared_gpu && !search ? 1024 : 0), dd, prep),
+                  "hr_init");
         init = ws.init.as<double>();
         init_status = ws.hr_status.as<int32_t>();
+    } else {
+        RCCHK(h, sts::launch_fit_prep(prep, s), "fit_prep");
     }
     if (ev_mid) HIPCHK(h, hipEventRecord(ev_mid, s));
     if (method == ARIMA_METHOD_CSS_BOBYQA && k > 0) {           // fitWithCSSBOBYQA, ARIMA.scala:106, :130-160
@@ -745,6 +795,11 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
         hipLaunchKernelGGL(k_fill_status, dim3(grid), dim3(256), 0, s, N, k, init_status, code, d_coef, d_ll,
                            d_status, d_neval, d_ngrad, d_flags);
         HIPCHK(h, hipGetLastError());
+        return ARIMA_OK;
+    }
+    if (gen) {                                                  // fitWithCSSCGD at runtime orders, a lane per series
+        RCCHK(h, sts::launch_gen_fit(y, ldn, n, N, p, q, I, h->smear, init, init_status, d_coef, d_ll, d_status,
+                                     d_neval, d_ngrad, d_flags, ws.ctl.as<unsigned long long>(), dd, s), "gen_fit");
         return ARIMA_OK;
     }
     // one persistent workgroup per CU (4 waves x the kernel's optimizer slots), the last num_cus/16 of them express
@@ -763,16 +818,11 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
     const int per_block = std::max(1, sts::cg_fit_series_per_block(p, q, I));
     const int64_t need = (N + per_block - 1) / per_block;
     if (blocks > need) blocks = (int)need;
-    if (xblocks > 0 || h->merge_live > 0) {                   // the merge pool: the ring's upper 3/4
-        RCCHK(h, ws.xring.ensure(sts::kExpressRingBytes), "workspace");
-        RCCHK(h, ws.xready.ensure(sts::kExpressReadyBytes), "workspace");
-        HIPCHK(h, hipMemsetAsync(ws.xready.ptr, 0, sts::kExpressReadyBytes, s));
-    }
     *grid_out = blocks;
     *express_out = xcus;                    // in CUs, the unit of the "express_blocks" option
     RCCHK(h, sts::launch_cg_fit(y, ldn, n, N, p, q, I, h->smear, init, init_status, d_coef, d_ll, d_status, d_neval,
                                 d_ngrad, d_flags, ws.ctl.as<unsigned long long>(), blocks, xblocks,
-                                ws.xring.as<unsigned char>(), ws.xready.as<unsigned>(), shared_gpu ? 0 : 1, s),
+                                ws.xring.as<unsigned char>(), ws.xready.as<unsigned>(), shared_gpu ? 0 : 1, s, dd),
           "cg_fit");
     hipLaunchKernelGGL(k_fault_merge, dim3(1), dim3(64), 0, s, ws.ctl.as<unsigned long long>(),
                        h->dev_fault.as<unsigned long long>());
@@ -782,10 +832,10 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
 
 // Grow the workspaces of the first `count` contexts to an N x ldn batch with k parameters at once, so that no
 // workspace grows (hipFree synchronises the device) while fits of other contexts are in flight.
-static int reserve_fit_ws(arima_handle *h, int count, int64_t N, int64_t ldn, int k) {
+static int reserve_fit_ws(arima_handle *h, int count, int64_t N, int64_t ldn, int k, bool diff_ws = true) {
     for (int j = 0; j < count; ++j) {
         FitCtx &c = h->fctx[j];
-        RCCHK(h, c.diff.ensure((size_t)N * ldn * sizeof(double)), "workspace");
+        if (diff_ws) RCCHK(h, c.diff.ensure((size_t)N * ldn * sizeof(double)), "workspace");
         RCCHK(h, c.ws.init.ensure((size_t)N * std::max(k, 1) * sizeof(double)), "workspace");
         RCCHK(h, c.ws.hr_status.ensure((size_t)N * sizeof(int32_t)), "workspace");
         RCCHK(h, c.ws.ctl.ensure(kCtlWords * sizeof(unsigned long long)), "workspace");
@@ -811,24 +861,34 @@ static int fit_device_locked(arima_handle *h, FitCtx &c, int ci, int reserve, co
     HIPCHK(h, hipSetDevice(h->device));
     const int k = I + p + q;
     const int n = std::max(T - d, 0);
-    const int64_t ldn = row_stride(h, n);
     c.pending = PendingStats{};
     if (slot < 0) {
         h->stats = arima_fit_stats{};
         h->stats_ctx = ci;
     }
     if (N == 0) return ARIMA_OK;
+    // Fused differencing (round 6): css-cgd fits (and the AR-only shortcut) of d <= 1 read the caller's rows directly
+    // -- d = 0 as they are, d = 1 differenced inside every pass (arima_device.hpp stream_row) -- instead of a
+    // differenced copy written by k_difference (17 GB of HBM traffic per 1M x 1024 fit, a pipeline stage of its own,
+    // and an N x T workspace per fit context). d >= 2 and css-bobyqa keep the copy.
+    const bool fused = d <= 1 && (method == ARIMA_METHOD_CSS_CGD || (p > 0 && q == 0)) && !h->no_fuse;
+    const int64_t ldn = fused ? ld : row_stride(h, n);
+    const double *rows = fused ? d_series : nullptr;
 
     SliceSlot *ss = slot >= 0 ? &h->slot[slot] : nullptr;
     hipEvent_t *ev = ss ? ss->ev : c.ev;
     unsigned long long *ctl_dst = ss ? h->slot_ctl + (size_t)slot * kCtlWords : c.ctl_host;
-    RCCHK(h, reserve_fit_ws(h, reserve, N, ldn, k), "workspace");
+    RCCHK(h, reserve_fit_ws(h, reserve, N, ldn, k, !fused), "workspace");
     HIPCHK(h, hipEventRecord(ev[0], s));
-    RCCHK(h, sts::launch_difference(d_series, ld, c.diff.as<double>(), ldn, N, T, d, 1, s), "difference");
+    if (!fused) {
+        RCCHK(h, sts::launch_difference(d_series, ld, c.diff.as<double>(), ldn, N, T, d, 1, s), "difference");
+        rows = c.diff.as<double>();
+    }
     HIPCHK(h, hipEventRecord(ev[1], s));
     int64_t grid = 0, xblocks = 0;
-    RCCHK(h, fit_kernels(h, c.ws, c.diff.as<double>(), ldn, n, N, p, q, I, method, d_user_init, d_coef, d_ll,
-                         d_status, d_neval, d_ngrad, d_flags, s, ev[2], &grid, &xblocks, shared_gpu), "fit");
+    RCCHK(h, fit_kernels(h, c.ws, rows, ldn, n, N, p, q, I, method, d_user_init, d_coef, d_ll,
+                         d_status, d_neval, d_ngrad, d_flags, s, ev[2], &grid, &xblocks, shared_gpu, -2, false,
+                         fused ? d : 0), "fit");
     HIPCHK(h, hipEventRecord(ev[3], s));
     h->last_grid = grid;
     h->last_express = xblocks;
@@ -953,9 +1013,9 @@ int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_se
         FitCtx &c = h->fctx[ci];
         hipStream_t s = stream ? (hipStream_t)stream : c.stream;
         begin_fit(h, c, s);
-        hipEvent_t ev_call = nullptr;
-        if (P > 1)
-            ev_call = order_after_overlapping_fits(h, ci, call_spans(d_series, n_series, T, ld,
+        // hazards against in-flight fits of every context, whatever P is now: fits issued under a larger
+        // fit_pipeline may still run on other contexts
+        hipEvent_t ev_call = order_after_overlapping_fits(h, ci, call_spans(d_series, n_series, T, ld,
                                                                      include_intercept + p + q, d_user_init,
                                                                      d_coef_out, d_css_ll_out, d_status_out,
                                                                      d_n_eval_out, d_n_grad_out, d_flags_out), s);
@@ -998,9 +1058,7 @@ int arima_fit_batch_device(arima_handle *h, const double *d_series, int64_t n_se
         FitCtx &c = h->fctx[ci];
         hipStream_t s = stream ? (hipStream_t)stream : c.stream;
         begin_fit(h, c, s);
-        hipEvent_t ev_call = nullptr;
-        if (P > 1)
-            ev_call = order_after_overlapping_fits(
+        hipEvent_t ev_call = order_after_overlapping_fits(
                 h, ci, call_spans(d_series + f * ld, ns, T, ld, k, d_user_init ? d_user_init + f * k : nullptr,
                                   d_coef_out + f * k, d_css_ll_out + f, d_status_out + f,
                                   d_n_eval_out ? d_n_eval_out + f : nullptr, d_n_grad_out ? d_n_grad_out + f : nullptr,
@@ -1082,6 +1140,54 @@ static void acc_stats(arima_fit_stats &a, const arima_fit_stats &s) {
     }
 }
 
+// memcpy with `threads` host threads (the caller's pageable rows into a pinned block: one thread copies at a fraction
+// of the host's memory bandwidth, a PCIe Gen5 x16 link needs several)
+static void par_memcpy(void *dst, const void *src, size_t bytes, int threads) {
+    const size_t min_part = size_t(4) << 20;
+    const int t = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(threads, 1), bytes / min_part));
+    if (t <= 1) {
+        memcpy(dst, src, bytes);
+        return;
+    }
+    std::vector<std::thread> pool;
+    const size_t part = (bytes + t - 1) / t / 64 * 64 + 64;
+    for (int i = 0; i < t; ++i) {
+        const size_t off = (size_t)i * part;
+        if (off >= bytes) break;
+        const size_t len = std::min(part, bytes - off);
+        pool.emplace_back([=] { memcpy((char *)dst + off, (const char *)src + off, len); });
+    }
+    for (auto &th : pool) th.join();
+}
+
+// Host rows -> device on stream s through the handle's ring of pinned blocks: block i is filled by the copy threads
+// while block i-1's DMA runs; a block is refilled only after its previous DMA has finished (its event). The caller's
+// buffer is fully read when this returns (as a pageable hipMemcpyAsync's is).
+static int upload_staged(arima_handle *h, void *dst, const void *src, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return ARIMA_OK;
+    if (h->host_copy_threads <= 0) {
+        HIPCHK(h, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s));
+        return ARIMA_OK;
+    }
+    for (size_t off = 0; off < bytes;) {
+        const int j = (int)(h->stage_next++ % arima_handle::kStageSlots);
+        if (!h->stage[j]) {
+            if (hipHostMalloc(&h->stage[j], arima_handle::kStageBytes, 0) != hipSuccess)
+                return set_err(h, ARIMA_E_OOM, "pinned staging");
+            HIPCHK(h, hipEventCreateWithFlags(&h->stage_ev[j], hipEventDisableTiming));
+        } else if (h->stage_used[j]) {
+            HIPCHK(h, hipEventSynchronize(h->stage_ev[j]));
+        }
+        const size_t len = std::min(arima_handle::kStageBytes, bytes - off);
+        par_memcpy(h->stage[j], (const char *)src + off, len, h->host_copy_threads);
+        HIPCHK(h, hipMemcpyAsync((char *)dst + off, h->stage[j], len, hipMemcpyHostToDevice, s));
+        HIPCHK(h, hipEventRecord(h->stage_ev[j], s));
+        h->stage_used[j] = true;
+        off += len;
+    }
+    return ARIMA_OK;
+}
+
 // Wait for context c's chunk, copy its results to the caller's arrays and add its counters to h->host_acc.
 static int drain_chunk(arima_handle *h, FitCtx &c, int k, const HostOut &o) {
     if (c.chunk_n <= 0) return ARIMA_OK;
@@ -1154,9 +1260,8 @@ int arima_fit_batch(arima_handle *h, const double *series, int64_t N, int32_t T,
         const int64_t first = j * chunk, n = std::min(chunk, N - first);
         hipStream_t s = c.stream;
         begin_fit(h, c, s);
-        if (T > 0)
-            HIPCHK(h, hipMemcpyAsync(c.d_series.ptr, series + first * T, (size_t)n * T * sizeof(double),
-                                     hipMemcpyHostToDevice, s));
+        if (T > 0) RCCHK(h, upload_staged(h, c.d_series.ptr, series + first * T, (size_t)n * T * sizeof(double), s),
+                         "upload");
         const double *d_ui = nullptr;
         if (user_init) {
             if (k > 0)
@@ -1341,6 +1446,23 @@ int arima_model_flags_batch(arima_handle *h, const double *coef, int64_t N, int3
     return ARIMA_OK;
 }
 
+// ARIMAModel.forecast over a device batch: k_forecast (p, q <= 5, d <= 8, the streaming kernel) or the runtime-order
+// k_gen_forecast for every other order, in slices whose per-series arrays fit a bounded workspace (h->fc_ws)
+static int forecast_any(arima_handle *h, const double *ts, int64_t ld, const double *coef, int k, double *out,
+                        int64_t ld_out, int64_t N, int T, int p, int d, int q, int I, int n_future, hipStream_t s) {
+    if (!sts::gen_order(p, q) && d <= 8)
+        return sts::launch_forecast(ts, ld, coef, k, out, ld_out, N, T, p, d, q, I, n_future, s);
+    const int64_t w = sts::gen_forecast_ws_doubles(T, p, d, q, n_future);
+    const int64_t chunk = std::max<int64_t>(64, std::min<int64_t>(N, (int64_t(1) << 27) / std::max<int64_t>(w, 1)));
+    RCCHK(h, h->fc_ws.ensure((size_t)std::min(chunk, N) * w * sizeof(double)), "forecast workspace");
+    for (int64_t f = 0; f < N; f += chunk) {
+        const int64_t n = std::min(chunk, N - f);
+        RCCHK(h, sts::launch_gen_forecast(ts + f * ld, ld, coef + f * k, k, out + f * ld_out, ld_out, n, T, p, d, q, I,
+                                          n_future, h->fc_ws.as<double>(), w, s), "forecast");
+    }
+    return ARIMA_OK;
+}
+
 int arima_forecast_batch(arima_handle *h, const double *series, int64_t N, int32_t T, int32_t p, int32_t d,
                          int32_t q, int32_t I, const double *coef, int32_t n_future, double *out) {
     if (!h) return ARIMA_E_INVALID_ARG;
@@ -1359,7 +1481,7 @@ int arima_forecast_batch(arima_handle *h, const double *series, int64_t N, int32
     RCCHK(h, h->h_aux.ensure((size_t)N * std::max<int64_t>(L, 1) * sizeof(double)), "staging");
     if (T > 0) HIPCHK(h, hipMemcpyAsync(h->h_series.ptr, series, (size_t)N * T * sizeof(double), hipMemcpyHostToDevice, s));
     if (k > 0) HIPCHK(h, hipMemcpyAsync(h->h_coef.ptr, coef, (size_t)N * k * sizeof(double), hipMemcpyHostToDevice, s));
-    RCCHK(h, sts::launch_forecast(h->h_series.as<double>(), T, h->h_coef.as<double>(), k, h->h_aux.as<double>(), L, N,
+    RCCHK(h, forecast_any(h, h->h_series.as<double>(), T, h->h_coef.as<double>(), k, h->h_aux.as<double>(), L, N,
                                   T, p, d, q, I, n_future, s), "forecast");
     if (L > 0) HIPCHK(h, hipMemcpyAsync(out, h->h_aux.ptr, (size_t)N * L * sizeof(double), hipMemcpyDeviceToHost, s));
     HIPCHK(h, end_call(h, s));
@@ -1380,7 +1502,7 @@ int arima_forecast_batch_device(arima_handle *h, const double *d_series, int64_t
     HIPCHK(h, hipSetDevice(h->device));
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     begin_call(h, s);
-    RCCHK(h, sts::launch_forecast(d_series, ld, d_coef, I + p + q, d_out, ld_out, N, T, p, d, q, I, n_future, s),
+    RCCHK(h, forecast_any(h, d_series, ld, d_coef, I + p + q, d_out, ld_out, N, T, p, d, q, I, n_future, s),
           "forecast");
     HIPCHK(h, end_call(h, s));
     return ARIMA_OK;
@@ -1651,29 +1773,20 @@ int arima_order_search_batch(arima_handle *h, const double *series, int64_t N, i
 // The walk ends when no series has candidates left (at most max_p + 2 rounds after the first).
 constexpr int kAfContexts = 4;                     // fit contexts the orders of one round rotate over
 
-static int autofit_locked(arima_handle *h, const double *d_series, int64_t N, int32_t T, int64_t ld, int32_t max_p,
-                          int32_t max_d, int32_t max_q, int32_t *d_order, double *d_coef, double *d_aic,
-                          int32_t *d_status, int32_t *d_nfits, hipStream_t s, int64_t *fits_out) {
-    using sts::kAfCombos;
-    if (max_p < 0 || max_q < 0 || max_d < 0) return set_err(h, ARIMA_E_INVALID_ARG, "bad autofit bounds");
-    if (max_p > 5 || max_q > 5 || max_d > kMaxD) return set_err(h, ARIMA_E_UNSUPPORTED, "p, q <= 5, d <= 16");
-    if (N < 0 || T < 0 || ld < T || (N > 0 && (!d_series || !d_order || !d_coef || !d_aic || !d_status)))
-        return set_err(h, ARIMA_E_INVALID_ARG, "bad shape");
-    h->stats = arima_fit_stats{};
-    h->stats_ctx = -1;
-    if (N == 0) return ARIMA_OK;
-    if (sts::kpss_lag_host(T) > sts::kpss_lag_max())
-        return set_err(h, ARIMA_E_UNSUPPORTED, "KPSS lag > 32 (series longer than ~19 900 points)");
-    HIPCHK(h, hipSetDevice(h->device));
+// One slice of the batch (every workspace sized for N series of length T). max_p <= sts::kAfMaxP.
+static int autofit_slice(arima_handle *h, const double *d_series, int64_t N, int32_t T, int64_t ld, int32_t max_p,
+                         int32_t max_d, int32_t max_q, int32_t *d_order, double *d_coef, double *d_aic,
+                         int32_t *d_status, int32_t *d_nfits, hipStream_t s, int64_t *fits_out) {
+    const int ncombos = sts::af_combos(max_p);
     const int64_t ldT = row_stride(h, T);
     const int64_t rows_max = N * sts::kAfMaxCand;  // candidate fits of one round, at most
     RCCHK(h, h->af_rows.ensure((size_t)N * ldT * sizeof(double)), "autofit workspace");
     RCCHK(h, h->af_dsel.ensure((size_t)N * sizeof(int32_t)), "autofit workspace");
     RCCHK(h, h->af_state.ensure((size_t)N * sizeof(sts::AfSeries)), "autofit workspace");
     RCCHK(h, h->af_best.ensure((size_t)N * 11 * sizeof(double)), "autofit workspace");
-    RCCHK(h, h->af_counts.ensure(kAfCombos * sizeof(unsigned)), "autofit workspace");
-    RCCHK(h, h->af_off.ensure(kAfCombos * sizeof(int64_t)), "autofit workspace");
-    RCCHK(h, h->af_lists.ensure((size_t)kAfCombos * N * sizeof(int32_t)), "autofit workspace");
+    RCCHK(h, h->af_counts.ensure(sts::kAfCombosMax * sizeof(unsigned)), "autofit workspace");
+    RCCHK(h, h->af_off.ensure(sts::kAfCombosMax * sizeof(int64_t)), "autofit workspace");
+    RCCHK(h, h->af_lists.ensure((size_t)ncombos * N * sizeof(int32_t)), "autofit workspace");
     RCCHK(h, h->af_coef.ensure((size_t)rows_max * 11 * sizeof(double)), "autofit workspace");
     RCCHK(h, h->af_ll.ensure((size_t)rows_max * sizeof(double)), "autofit workspace");
     RCCHK(h, h->af_status.ensure((size_t)rows_max * sizeof(int32_t)), "autofit workspace");
@@ -1682,7 +1795,7 @@ static int autofit_locked(arima_handle *h, const double *d_series, int64_t N, in
     RCCHK(h, h->af_hrst.ensure((size_t)rows_max * sizeof(int32_t)), "autofit workspace");
     RCCHK(h, h->af_rlist.ensure((size_t)rows_max * sizeof(int32_t)), "autofit workspace");
     RCCHK(h, h->af_rcount.ensure(sizeof(unsigned)), "autofit workspace");
-    if (!h->af_host && hipHostMalloc((void **)&h->af_host, 2 * kAfCombos * sizeof(int64_t), 0) != hipSuccess)
+    if (!h->af_host && hipHostMalloc((void **)&h->af_host, (2 * sts::kAfCombosMax + 1) * sizeof(int64_t), 0) != hipSuccess)
         return set_err(h, ARIMA_E_OOM, "pinned");
     if (!h->ev_af) HIPCHK(h, hipEventCreateWithFlags(&h->ev_af, hipEventDisableTiming));
     const int P = std::min(kAfContexts, kMaxPipeline);
@@ -1696,7 +1809,6 @@ static int autofit_locked(arima_handle *h, const double *d_series, int64_t N, in
         RCCHK(h, c.ws.xready.ensure(sts::kExpressReadyBytes), "workspace");
         if (c.has_done) HIPCHK(h, hipStreamWaitEvent(s, c.ev_done, 0));
     }
-    HIPCHK(h, hipEventRecord(h->ev[0], s));
     // (1) d: the first of 0..max_d whose differencesOfOrderD(ts, d) passes kpsstest(_, "c") (ARIMA.scala:287-297)
     const int32_t kpss_st = T <= 0 ? ARIMA_ST_NO_DATA : (T < 2 ? ARIMA_ST_NOT_ENOUGH_DATA : ARIMA_ST_OK);
     int32_t *dsel = h->af_dsel.as<int32_t>();
@@ -1713,28 +1825,28 @@ static int autofit_locked(arima_handle *h, const double *d_series, int64_t N, in
     RCCHK(h, sts::launch_af_init(N, dsel, st, kpss_st, s), "autofit init");
     int64_t fits = 0;
     for (int round = 0; kpss_st == ARIMA_ST_OK; ++round) {
-        HIPCHK(h, hipMemsetAsync(h->af_counts.ptr, 0, kAfCombos * sizeof(unsigned), s));
+        HIPCHK(h, hipMemsetAsync(h->af_counts.ptr, 0, ncombos * sizeof(unsigned), s));
         RCCHK(h, sts::launch_af_plan(N, st, h->af_counts.as<unsigned>(), h->af_lists.as<int32_t>(), s), "autofit plan");
-        unsigned counts[kAfCombos];
-        HIPCHK(h, hipMemcpyAsync(h->af_host, h->af_counts.ptr, kAfCombos * sizeof(unsigned), hipMemcpyDeviceToHost, s));
+        unsigned counts[sts::kAfCombosMax];
+        HIPCHK(h, hipMemcpyAsync(h->af_host, h->af_counts.ptr, ncombos * sizeof(unsigned), hipMemcpyDeviceToHost, s));
         HIPCHK(h, hipStreamSynchronize(s));
-        memcpy(counts, h->af_host, sizeof counts);
-        int64_t *off = h->af_host + kAfCombos;
+        memcpy(counts, h->af_host, ncombos * sizeof(unsigned));
+        int64_t *off = h->af_host + sts::kAfCombosMax;
         int64_t total = 0;
-        for (int cb = 0; cb < kAfCombos; ++cb) {
+        for (int cb = 0; cb < ncombos; ++cb) {
             off[cb] = total;
             total += counts[cb];
         }
         if (total == 0) break;
         fits += total;
-        HIPCHK(h, hipMemcpyAsync(h->af_off.ptr, off, kAfCombos * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        HIPCHK(h, hipMemcpyAsync(h->af_off.ptr, off, ncombos * sizeof(int64_t), hipMemcpyHostToDevice, s));
         HIPCHK(h, hipEventRecord(h->ev_af, s));
         // the round's orders, largest list first, over the fit contexts (several orders fit at once)
-        int order[kAfCombos];
-        for (int cb = 0; cb < kAfCombos; ++cb) order[cb] = cb;
-        std::stable_sort(order, order + kAfCombos, [&](int a, int b) { return counts[a] > counts[b]; });
+        int order[sts::kAfCombosMax];
+        for (int cb = 0; cb < ncombos; ++cb) order[cb] = cb;
+        std::stable_sort(order, order + ncombos, [&](int a, int b) { return counts[a] > counts[b]; });
         int used = 0;
-        for (int oi = 0; oi < kAfCombos && counts[order[oi]] > 0; ++oi) {
+        for (int oi = 0; oi < ncombos && counts[order[oi]] > 0; ++oi) {
             const int cb = order[oi];
             const int p = (cb / 2) / 3, q = (cb / 2) % 3, I = cb % 2;
             const int64_t cnt = counts[cb];
@@ -1743,7 +1855,8 @@ static int autofit_locked(arima_handle *h, const double *d_series, int64_t N, in
             RCCHK(h, sts::launch_gather_rows(h->af_rows.as<double>(), ldT, h->af_lists.as<int32_t>() + (int64_t)cb * N,
                                              cnt, T, c.diff.as<double>(), c.stream), "gather");
             int64_t gridb = 0, xb = 0;
-            // fitModel(p, 0, q, diffedTs, intercept, "css-cgd") (:316); rows of order cb from off[cb] (coef stride k)
+            // fitModel(p, 0, q, diffedTs, intercept, "css-cgd") (:316); rows of order cb from off[cb] (coef stride k);
+            // p > 5: the runtime-order path (fit_kernels dispatches it)
             RCCHK(h, fit_kernels(h, c.ws, c.diff.as<double>(), ldT, T, cnt, p, q, I, ARIMA_METHOD_CSS_CGD, nullptr,
                                  h->af_coef.as<double>() + off[cb] * 11, h->af_ll.as<double>() + off[cb],
                                  h->af_status.as<int32_t>() + off[cb], nullptr, nullptr,
@@ -1762,13 +1875,21 @@ static int autofit_locked(arima_handle *h, const double *d_series, int64_t N, in
         }
         for (int j = 0; j < std::min(used, P); ++j) HIPCHK(h, hipStreamWaitEvent(s, h->fctx[j].ev_done, 0));
         // fitTryBothStrategies (:315-319): every row of the round whose css-cgd fit threw in the optimizer, refitted
-        // with css-bobyqa from the same Hannan-Rissanen init, in place -- one launch for all the round's orders
-        RCCHK(h, sts::launch_bobyqa_refit_round(h->af_rows.as<double>(), ldT, T, h->af_lists.as<int32_t>(), N,
-                                                h->af_off.as<int64_t>(), total, h->af_init.as<double>(),
-                                                h->af_hrst.as<int32_t>(), h->af_rlist.as<int32_t>(),
-                                                h->af_rcount.as<unsigned>(), h->af_coef.as<double>(),
-                                                h->af_ll.as<double>(), h->af_status.as<int32_t>(),
-                                                h->af_flags.as<uint8_t>(), h->bobyqa_wave != 0, s), "bobyqa refit");
+        // with css-bobyqa from the same Hannan-Rissanen init, in place -- one launch for all the round's orders, sized
+        // by the retry count read back (one workgroup per retry, not per candidate row)
+        RCCHK(h, sts::launch_bobyqa_refit_list(h->af_off.as<int64_t>(), ncombos, total, h->af_status.as<int32_t>(),
+                                               h->af_rlist.as<int32_t>(), h->af_rcount.as<unsigned>(), s), "bobyqa list");
+        HIPCHK(h, hipMemcpyAsync(h->af_host + 2 * sts::kAfCombosMax, h->af_rcount.ptr, sizeof(unsigned),
+                                 hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipStreamSynchronize(s));
+        unsigned retries = 0;
+        memcpy(&retries, h->af_host + 2 * sts::kAfCombosMax, sizeof retries);
+        RCCHK(h, sts::launch_bobyqa_refit_rows(h->af_rows.as<double>(), ldT, T, h->af_lists.as<int32_t>(), N,
+                                               h->af_off.as<int64_t>(), ncombos, 11, h->af_rlist.as<int32_t>(),
+                                               h->af_rcount.as<unsigned>(), (int64_t)retries, h->af_init.as<double>(),
+                                               h->af_hrst.as<int32_t>(), h->af_coef.as<double>(),
+                                               h->af_ll.as<double>(), h->af_status.as<int32_t>(),
+                                               h->af_flags.as<uint8_t>(), h->bobyqa_wave != 0, s), "bobyqa refit");
         RCCHK(h, sts::launch_af_update(N, st, h->af_off.as<int64_t>(), h->af_coef.as<double>(), h->af_ll.as<double>(),
                                        h->af_status.as<int32_t>(), h->af_flags.as<uint8_t>(), h->af_best.as<double>(),
                                        max_p, max_q, s), "autofit update");
@@ -1776,6 +1897,45 @@ static int autofit_locked(arima_handle *h, const double *d_series, int64_t N, in
     }
     RCCHK(h, sts::launch_af_finish(N, st, h->af_best.as<double>(), d_order, d_coef, d_aic, d_status, d_nfits, s),
           "autofit finish");
+    if (fits_out) *fits_out = fits;
+    return ARIMA_OK;
+}
+
+// ARIMA.autoFit over the batch in slices whose workspaces fit the free HBM (the per-call footprint is ~5x
+// the input -- the differenced rows plus one gather buffer per fit context -- so a large batch is cut instead of
+// failing with ARIMA_E_OOM); option "autofit_slice" fixes the slice (series), 0 = from free HBM.
+static int autofit_locked(arima_handle *h, const double *d_series, int64_t N, int32_t T, int64_t ld, int32_t max_p,
+                          int32_t max_d, int32_t max_q, int32_t *d_order, double *d_coef, double *d_aic,
+                          int32_t *d_status, int32_t *d_nfits, hipStream_t s, int64_t *fits_out) {
+    if (max_p < 0 || max_q < 0 || max_d < 0) return set_err(h, ARIMA_E_INVALID_ARG, "bad autofit bounds");
+    if (max_p > sts::kAfMaxP || max_d > kMaxD)
+        return set_err(h, ARIMA_E_UNSUPPORTED, "autofit: max_p <= 8 (css-bobyqa retries of <= 11 parameters), d <= 16");
+    if (N < 0 || T < 0 || ld < T || (N > 0 && (!d_series || !d_order || !d_coef || !d_aic || !d_status)))
+        return set_err(h, ARIMA_E_INVALID_ARG, "bad shape");
+    h->stats = arima_fit_stats{};
+    h->stats_ctx = -1;
+    if (N == 0) return ARIMA_OK;
+    HIPCHK(h, hipSetDevice(h->device));
+    const int64_t ldT = row_stride(h, T);
+    int64_t slice = h->autofit_slice;
+    if (slice <= 0) {
+        size_t free_b = 0, total_b = 0;
+        HIPCHK(h, hipMemGetInfo(&free_b, &total_b));
+        size_t held = h->af_rows.bytes;            // workspaces this call reuses
+        for (int j = 0; j < kAfContexts; ++j) held += h->fctx[j].diff.bytes;
+        const int64_t per = (int64_t)(1 + kAfContexts) * ldT * 8 + sts::kAfMaxCand * (11 * 16 + 16) +
+                            (int64_t)sts::kAfCombosMax * 4 + 256;
+        slice = std::max<int64_t>(4096, (int64_t)((free_b + held) / 10 * 6) / per);
+    }
+    HIPCHK(h, hipEventRecord(h->ev[0], s));
+    int64_t fits = 0;
+    for (int64_t f = 0; f < N; f += slice) {
+        const int64_t n = std::min(slice, N - f);
+        int64_t fs = 0;
+        RCCHK(h, autofit_slice(h, d_series + f * ld, n, T, ld, max_p, max_d, max_q, d_order + f * 4, d_coef + f * 11,
+                               d_aic + f, d_status + f, d_nfits ? d_nfits + f : nullptr, s, &fs), "autofit");
+        fits += fs;
+    }
     HIPCHK(h, hipEventRecord(h->ev[3], s));
     h->stats.n_series = fits;
     if (fits_out) *fits_out = fits;
@@ -1788,12 +1948,17 @@ int arima_autofit_batch_device(arima_handle *h, const double *d_series, int64_t 
                                void *stream) {
     if (!h) return ARIMA_E_INVALID_ARG;
     std::lock_guard<std::mutex> lk(h->mu);
+    HIPCHK(h, hipSetDevice(h->device));          // before any stream work
     hipStream_t s = stream ? (hipStream_t)stream : h->stream;
     begin_call(h, s);
     const int rc = autofit_locked(h, d_series, n_series, T, ld, max_p, max_d, max_q, d_order_out, d_coef_out,
                                   d_aic_out, d_status_out, d_n_fits_out, s, nullptr);
     HIPCHK(h, end_call(h, s));
-    return rc;
+    // the walk synchronised with the device once per round, so its fits have finished: a watchdog fault that one of
+    // them recorded is reported by this call, not by a later unrelated one
+    if (rc != ARIMA_OK) return rc;
+    HIPCHK(h, hipStreamSynchronize(s));
+    return take_fault(h);
 }
 
 int arima_autofit_batch(arima_handle *h, const double *series, int64_t N, int32_t T, int32_t max_p, int32_t max_d,
@@ -1837,8 +2002,6 @@ int arima_kpss_batch(arima_handle *h, const double *series, int64_t N, int32_t T
     if (N == 0) return ARIMA_OK;
     if (!series || !stat_out || !status_out) return set_err(h, ARIMA_E_INVALID_ARG, "null buffer");
     const int32_t st = T <= 0 ? ARIMA_ST_NO_DATA : (T < 2 ? ARIMA_ST_NOT_ENOUGH_DATA : ARIMA_ST_OK);
-    if (st == ARIMA_ST_OK && sts::kpss_lag_host(T) > sts::kpss_lag_max())
-        return set_err(h, ARIMA_E_UNSUPPORTED, "KPSS lag > 32 (series longer than ~19 900 points)");
     HIPCHK(h, hipSetDevice(h->device));
     hipStream_t s = h->stream;
     begin_call(h, s);

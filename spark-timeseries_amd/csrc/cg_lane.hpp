@@ -121,10 +121,24 @@ STS_HD STS_FI bool brent_first_u(double A, double B, double C, double &u) {
 // taken) until the interval is below tolerance. tests/test_cglane_sim.py steps the machine to check the constant.
 constexpr int kNanIterEvals = 77;
 
+// The parameter count n = point.length of the optimizer: the conjugate-gradient restart period (`iter % n == 0`).
+// KDim: the compile-time K of the order-specialised kernels (no storage); RuntimeDim: the runtime-order path
+// (arima_generic.hip), whose lanes hold K = kGenMaxK padded coordinates of which the first kdim are the fit's --
+// every other operation of the machine leaves zero padding exact (a dot product gains + 0.0 terms, a padded
+// coordinate of a non-finite point is non-finite only when a real one is).
+template <int K>
+struct KDim {
+    STS_HD STS_FI int dim() const { return K; }
+};
+struct RuntimeDim {
+    int32_t kdim;
+    STS_HD STS_FI int dim() const { return kdim; }
+};
+
 // NS: predicted alphas posted with one F request; NC: values cached per line search. FF: fast-forward the
 // NaN-absorbing state in closed form (PC_TOP below); false only in the CPU simulator, to check kNanIterEvals.
-template <int K, int NS_, int NC_, bool FF = true>
-struct CGLane {
+template <int K, int NS_, int NC_, bool FF = true, class DimT = KDim<K>>
+struct CGLane : DimT {
     static constexpr int NS = NS_;
     static constexpr int NC = NC_;
     static constexpr int NS1 = NS > 0 ? NS : 1;
@@ -557,7 +571,7 @@ struct CGLane {
                 for (int i = 0; i < K; ++i) dl = dl + grad[i] * grad[i];
                 delta = dl;
                 const double beta = delta / deltaOld;       // FLETCHER_REEVES
-                if (iter % K == 0 || beta < 0) {
+                if (iter % this->dim() == 0 || beta < 0) {
 #pragma unroll
                     for (int i = 0; i < K; ++i) dir[i] = grad[i];
                 } else {

@@ -78,7 +78,7 @@ def test_autofit_device_entry_point_and_bounds(engine):
                           out["aic"].data_ptr(), out["status"].data_ptr(), out["n_fits"].data_ptr())
     check_autofit({k: v.cpu().numpy() for k, v in out.items()}, arr, "device entry point")
     with pytest.raises(Exception):
-        engine.autofit(arr["series"], 6, 2, 5)                       # p <= 5 compiled
+        engine.autofit(arr["series"], 9, 2, 5)     # max_p <= 8: its css-bobyqa retries have <= 11 parameters
 
 
 def test_autofit_long_series_matches_oracle(engine):

@@ -58,7 +58,7 @@ def test_bench_two_ranks_on_one_gpu_checks_every_rank_against_the_oracle():
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", OMP_NUM_THREADS="4")
     env.pop("WORLD_SIZE", None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--device", "0", "--series", "16384",
-           "--steps", "2", "--warmup", "1", "--e2e", "0", "--cpu-seconds", "2", "--pipeline", "2"]
+           "--steps", "2", "--warmup", "1", "--e2e", "1", "--cpu-seconds", "2", "--pipeline", "2"]
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -69,6 +69,12 @@ def test_bench_two_ranks_on_one_gpu_checks_every_rank_against_the_oracle():
     assert par["oracle_rows"] >= 2 * 256 and par["bit_identical"] == par["oracle_rows"]
     assert par["every_rank_bit_identical"] and par["min_rank_fraction"] == 1.0 and par["vs_isolated"]
     assert line["cpu_baseline"] is None                     # the CPU baseline is timed at N = 1 only
+    # the host-memory leg on every rank at once: both ranks' uploads, results equal to the device
+    # path on every row of every rank
+    e2e = line["end_to_end_host"]
+    assert e2e["n_ranks"] == 2 and e2e["series"] == 2 * 16384 and e2e["rows_compared"] == 2 * 16384
+    assert e2e["bit_identical_to_device_path"] and e2e["rows_identical"] == e2e["rows_compared"]
+    assert e2e["value"] > 0 and e2e["GBps_in"] > 0
 
 
 def test_bench_autofit_two_ranks_on_one_gpu_checks_every_rank():

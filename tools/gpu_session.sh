@@ -5,16 +5,16 @@
 #   SMOKE=1        __graft_entry__.smoke()                -> $OUT/smoke.log
 #   BENCH="args"   python bench.py <args>                 -> $OUT/bench.json (+ .err)   (BENCH2/BENCH3 likewise)
 #   PROF=1         tools/profile.sh (kernel trace + PMC passes of the C2 bench; CONFIG/SER as there) -> $OUT/prof
-# OUT defaults to gpurun_out/r05/<TAG>. Every record kept under profiles/ names the TAG of the session it came from.
+# OUT defaults to gpurun_out/r06/<TAG>. Every record kept under profiles/ names the TAG of the session it came from.
 cd /tmp && export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-OUT=gpurun_out/r05/${TAG:-s}
+OUT=gpurun_out/r06/${TAG:-s}
 mkdir -p "$OUT"
 sha256sum spark-timeseries_amd/libsparkts_arima.so > "$OUT/library.sha256"
 ok=0
 run_tests() {
     [ "${TESTS:-0}" = 1 ] || return 0
-    timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread ${SEL:+-k "$SEL"} \
+    timeout -k 10 ${TEST_TIMEOUT:-600} python -u -m pytest tests -m gpu -x -q --timeout 180 --timeout-method thread ${SEL:+-k "$SEL"} \
         > "$OUT/pytest_gpu.log" 2>&1
 }
 run_smoke() {
