@@ -62,9 +62,9 @@ CONFIGS = {
     "c1": (1, 0, 1, 1, 500, [3.5, 0.3, 0.7], 0.05),
     "c4": (5, 1, 5, 1, 4096, [0.1, 0.4, -0.2, 0.1, 0.05, -0.05, 0.3, 0.2, -0.1, 0.05, 0.05], 0.05),
 }
-# configs[0]: 10k series; autoFit 64k (each of its ~7 rounds waits for its slowest css-bobyqa retry: 38 s per 64k
-# series, profiles/r05/j_css); every other config 1M per GPU
-DEFAULT_SERIES = {"c1": 10000, "af": 1 << 16}
+# configs[0]: 10k series; every other config 1M per GPU (autoFit too since round 6: each of its ~7 rounds waits for
+# its slowest css-bobyqa retry, which a 1M batch amortises -- 34.7k series/s at 1M vs 7.7k at 64k, profiles/r06/e_split)
+DEFAULT_SERIES = {"c1": 10000}
 METRICS = {
     "c2": "series fitted/sec, ARIMA(2,1,2) CSS-CGD, 1M x 1024 pts",
     "c1": "series fitted/sec, ARIMA(1,0,1) CSS-CGD, 10k x 500 pts (BASELINE.json configs[0])",
@@ -431,7 +431,7 @@ def main():
 
     p, d, q, I, T, base, jitter = CONFIGS[args.config]
     if args.steps is None:                  # enough steps that the pipeline's fill is amortised (C2: 3 steps read
-        args.steps = {"c4": 5, "c5": 2, "af": 2}.get(args.config, 20)   # 9.35 M series/s, 20 steps 11.0, profiles/r04/zz_check)
+        args.steps = {"c4": 5, "c5": 2, "af": 1}.get(args.config, 20)   # 9.35 M series/s, 20 steps 11.0, profiles/r04/zz_check)
     if args.warmup is None:
         args.warmup = 1 if args.config in ("c5", "af") else 3
     if args.pipeline <= 0:

@@ -137,7 +137,8 @@ int         arima_synchronize(arima_handle *h);
  * parameters (the dimensions its kernels compile) and autoFit with max_p > 8 (its css-bobyqa retries).
  * Tuning knobs (not part of the reference contract): "smear" (Breeze reading at ARIMA.scala:526, default 1),
  * "fit_pipeline" (fit contexts in rotation for *_device fits, 1..8, default 3), "host_chunk" / "host_pipeline"
- * (series per chunk and contexts of the chunked host path, default 262144 / 3), "express_blocks",
+ * (series per chunk and contexts of the chunked host path: 131072 / 6 when GPU_MAX_HW_QUEUES >= 8 at arima_create, else
+ * 262144 / 3), "host_tail" (1: the host path halves its last chunks), "express_blocks",
  * "grid_blocks", "search_lanes" (in-kernel scheduler and order-search concurrency), "hr_grid" (k_hr_init grid:
  * 0 = a lane per series, > 0 = that
  * many single-wave workgroups, -1 = 1024 for pipelined fits else 0), "fit_slice_bytes"
@@ -150,7 +151,8 @@ int         arima_synchronize(arima_handle *h);
  * the batch's work counter ran out; 0 = the kernel's 256 / 32), "fuse_diff" (1, default: device fits of d <= 1 read the
  * caller's rows and difference them inside every pass; 0: through a k_difference workspace -- identical results),
  * "autofit_slice" (autoFit series per slice of its workspaces, 0 = from free HBM), "host_copy_threads" (host threads
- * that copy arima_fit_batch's rows into pinned blocks for the upload, default 8; 0 = upload from pageable memory). */
+ * that copy arima_fit_batch's rows into pinned blocks for the upload; default 0 = upload from pageable memory through
+ * the HIP runtime's staging), "chain_overhead" (k_cg_fit's objective-pass width model; 0 = the kernel's). */
 int         arima_set_option(arima_handle *h, const char *name, int64_t value);
 /* Current value of a tuning knob (the names arima_set_option takes); ARIMA_E_INVALID_ARG for an unknown name. */
 int         arima_get_option(const arima_handle *h, const char *name, int64_t *value);

@@ -1,0 +1,6 @@
+// css-bobyqa kernels of dimension 9 (arima_bobyqa_impl.hpp), one translation unit per dimension
+#include "arima_bobyqa_impl.hpp"
+
+namespace sts {
+STS_BQ_DECLARE(9, )
+}  // namespace sts

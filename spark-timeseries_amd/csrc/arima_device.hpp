@@ -1026,6 +1026,7 @@ __device__ __forceinline__ void fit_prep(const FitPrep &fp) {
         else if (g == 44) v = fp.v44;            // drain merge threshold ("merge_live")
         else if (g == 45) v = fp.v45;            // donation thresholds ("donate_evals", "donate_evals_drained")
         else if (g == 46) v = fp.v46;
+        else if (g == 47) v = fp.v47;            // objective-pass width model ("chain_overhead")
         fp.ctl[g] = v;
     }
     for (int64_t i = g; i < fp.xready_words; i += stride) fp.xready[i] = 0u;

@@ -625,6 +625,9 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
     // sees every reserved entry claimed -- so while entries are unclaimed some active wave remains to take them.
     // Only where a series is fitted changes, never its result.
     const int merge_live = (int)ctl[44];
+    // objective-pass width model: per-step streaming cost of a pass in 1/16 chains (ctl[47], option "chain_overhead";
+    // 0 = kChainOverhead16). A larger value prices bytes higher and so prefers wider passes (more chains per row read)
+    const int chain_ovh = ctl[47] ? (int)ctl[47] : kChainOverhead16;
     unsigned char *mpool = xq + (size_t)(kExpressRing - kMergeCap) * kExpressEntryBytes;
     unsigned *mready = xready + (kExpressRing - kMergeCap);
     unsigned long long merge_head = 0;     // entries claimed, as last seen (a lower bound)
@@ -882,7 +885,7 @@ __global__ __launch_bounds__(64 * kFitWaves) __attribute__((amdgpu_waves_per_eu(
                 t = n2 < left ? n2 : left; u += t * (c < 3 ? c : 3); left -= t;
                 t = n1 < left ? n1 : left; u += t * (c < 2 ? c : 2); left -= t;
                 t = n0 < left ? n0 : left; u += t; left -= t;
-                const int score = u * 4096 / (kChainOverhead16 + 16 * c);
+                const int score = u * 4096 / (chain_ovh + 16 * c);
                 if (score >= best) { best = score; nchc = c; }
             }
         }

@@ -26,14 +26,14 @@ int launch_forecast(const double *ts, int64_t ld_in, const double *coef, int k, 
 int launch_inverse_difference(const double *in, int64_t ld_in, double *out, int64_t ld_out, int64_t N, int T,
                               int d, hipStream_t s);
 // The fit kernel's counter words (ctl) and express-ring ready words are initialised by the kernel that runs before it
-// on the same stream (k_hr_init, else k_fit_prep): ctl[] = 0 except ctl[15] = ~0 and the option words 19, 44, 45, 46;
+// on the same stream (k_hr_init, else k_fit_prep): ctl[] = 0 except ctl[15] = ~0 and the option words 19, 44-47;
 // xready[0 .. xready_words) = 0. ctl == nullptr / xready_words == 0: nothing to prepare.
 constexpr int kFitCtlWords = 48;
 struct FitPrep {
     unsigned long long *ctl = nullptr;
     unsigned *xready = nullptr;
     int64_t xready_words = 0;
-    unsigned long long v19 = 0, v44 = 0, v45 = 0, v46 = 0;
+    unsigned long long v19 = 0, v44 = 0, v45 = 0, v46 = 0, v47 = 0;
 };
 int launch_fit_prep(const FitPrep &prep, hipStream_t s);
 // hr_grid > 0: that many single-wave workgroups stride over the series (bounds the rows in flight, so the 2(C_A + C_B)
@@ -115,14 +115,16 @@ int launch_bobyqa_fit(const double *y, int64_t ld, int n, int64_t N, int p, int 
 // autoFit: the css-bobyqa retries of a whole round (every order's rows whose css-cgd fit threw in the optimizer), one
 // launch; rows = the differenced series (ld), lists / off = the round's per-order lists and row offsets, init /
 // init_status = each row's Hannan-Rissanen init (k-strided from off[cb] * 11) and status; list / count: workspace
-// (two launches: the list, whose length the host reads back, then one retry per listed row; ncombos orders in the
-// round's layout, coefficient rows kc-strided from off[cb] * kc)
+// (the list, bucketed by dimension k = p + q + intercept -- bucket k at list[k * stride ..], counts[k] rows -- then
+// one kernel per dimension present, each on its own stream; ncombos orders in the round's layout, coefficient rows
+// kc-strided from off[cb] * kc)
+constexpr int kBqRefitBuckets = 12;
 int launch_bobyqa_refit_list(const int64_t *off, int ncombos, int64_t total, const int32_t *status, int32_t *list,
-                             unsigned *count, hipStream_t s);
-int launch_bobyqa_refit_rows(const double *rows_, int64_t ld, int n, const int32_t *lists, int64_t N,
-                             const int64_t *off, int ncombos, int kc, const int32_t *list, const unsigned *count,
-                             int64_t rows, const double *init, const int32_t *init_status, double *coef, double *ll,
-                             int32_t *status, uint8_t *flags, bool wave, hipStream_t s);
+                             int64_t stride, unsigned *counts, hipStream_t s);
+int launch_bobyqa_refit_dim(int k, const double *rows_, int64_t ld, int n, const int32_t *lists, int64_t N,
+                            const int64_t *off, int ncombos, int kc, const int32_t *list, const unsigned *counts,
+                            int64_t rows, const double *init, const int32_t *init_status, double *coef, double *ll,
+                            int32_t *status, uint8_t *flags, bool wave, hipStream_t s);
 
 int hr_shape_status_host(int n, int p, int q, int I);
 int ar_shape_status_host(int n, int p, int I);

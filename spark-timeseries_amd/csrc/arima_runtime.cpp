@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -163,6 +164,7 @@ struct arima_handle {
     int search_express_blocks = 0;
     int donate_evals = 0;          // k_cg_fit: evaluations before a slot may go to an express wave (0: kernel default)
     int donate_evals_drained = 0;  // ... once the batch's work counter has run out (0: kernel default)
+    int chain_overhead = 0;        // k_cg_fit's objective-pass width model, 1/16 chains per step (0: kernel default 6)
     // k_hr_init: 0 = a lane per series; > 0 = that many single-wave workgroups (grid-stride); -1 (default) = 1 024
     // for pipelined device fits (fit_pipeline > 1: C2 9.47-9.55 -> 9.68-9.75 M series/s, profiles/r04/m_hrgrid),
     // else 0 (alone it is 25.2 vs 26.9 ms at C2)
@@ -190,13 +192,20 @@ struct arima_handle {
     // (Cutting ONE call into slices over several contexts was measured on the box's 4 queues at C2 1M x 1024 and
     // removed: 1 / 2 / 3 / 4 slices 6.91 / 6.39 / 6.35 / 4.47 M series/s, every slice ends with its own slowest
     // series; profiles/r05/c_af2/default_cs*.json.)
-    int host_pipeline = 3;         // contexts the chunked host path rotates over
-    int64_t host_chunk = 1 << 18;  // series per chunk of the host path (option "host_chunk")
-    // host path uploads (round 6): the caller's pageable rows are copied by host_copy_threads threads into a ring of
-    // pinned blocks, each block DMA'd to the device while the threads fill the next (upload_staged). Before, the
-    // uploads went straight from pageable memory through the HIP runtime's own staging: 32.6 GB/s on the box's
-    // PCIe Gen5 x16 (3.98 M series/s end to end at C2). Option "host_copy_threads" 0 restores it.
-    int host_copy_threads = 8;
+    // host path (arima_fit_batch): chunks of host_chunk series over host_pipeline fit contexts, the last ones halved
+    // (host_tail). C2 1M x 1024 from pageable memory, 8 hardware queues: 262144 x 3 contexts 3.86 M series/s,
+    // 131072 x 6 4.47-4.65, 65536 x 6 3.65 (profiles/r06/g_e2e); the upload runs at the link's 56 GB/s either way
+    // (tools/h2d_bw.py, profiles/r06/d_ab/h2d.json), so the call is bound by the uploads plus its last fit's tail
+    static constexpr int64_t kHostTailMin = 16384;
+    int host_pipeline = 3;         // contexts the chunked host path rotates over (option "host_pipeline"; arima_create)
+    int64_t host_chunk = 1 << 18;  // series per chunk of the host path (option "host_chunk"; arima_create)
+    int host_tail = 1;             // halve the last chunks (option "host_tail")
+    // host path uploads: with host_copy_threads > 0 the caller's pageable rows are copied by that many threads into a
+    // ring of pinned blocks, each block DMA'd while the threads fill the next (upload_staged); 0 (default) uploads
+    // straight from pageable memory through the HIP runtime's own staging. Both reach the link's ~56 GB/s on the box
+    // (tools/h2d_bw.py), and the runtime's staging measured slightly faster end to end (4.65 vs 4.47 M series/s at
+    // C2, profiles/r06/g_e2e), so the staged ring stays an option for hosts whose pageable path is slower.
+    int host_copy_threads = 0;
     static constexpr int kStageSlots = 3;
     static constexpr size_t kStageBytes = size_t(128) << 20;
     void *stage[kStageSlots] = {};
@@ -367,6 +376,15 @@ int arima_create(int device, arima_handle **out) {
     if (hipSetDevice(device) != hipSuccess) return ARIMA_E_DEVICE;
     arima_handle *h = new arima_handle();
     h->device = device;
+    // the host path's contexts need hardware queues of their own (HIP maps a process's streams onto
+    // GPU_MAX_HW_QUEUES of them, default 4): 6 contexts of 131072-series chunks with 8 or more queues, else 3 of 262144
+    // (profiles/r06/e_split, g_e2e: on 4 queues 4+ contexts serialise and run slower than 3)
+    if (const char *q = getenv("GPU_MAX_HW_QUEUES")) {
+        if (atoi(q) >= 8) {
+            h->host_pipeline = 6;
+            h->host_chunk = 1 << 17;
+        }
+    }
     hipDeviceGetAttribute(&h->num_cus, hipDeviceAttributeMultiprocessorCount, device);
     int rc = ARIMA_OK;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) rc = ARIMA_E_DEVICE;
@@ -567,6 +585,7 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
     if (!strcmp(name, "smear")) { h->smear = value ? 1 : 0; return ARIMA_OK; }
     if (!strcmp(name, "bobyqa_wave")) { h->bobyqa_wave = value < 0 ? -1 : (value ? 1 : 0); return ARIMA_OK; }
     if (!strcmp(name, "fuse_diff")) { h->no_fuse = value ? 0 : 1; return ARIMA_OK; }
+    if (!strcmp(name, "chain_overhead")) { h->chain_overhead = (int)std::min<int64_t>(4096, std::max<int64_t>(0, value)); return ARIMA_OK; }
     if (!strcmp(name, "autofit_slice")) { h->autofit_slice = std::max<int64_t>(0, value); return ARIMA_OK; }
     if (!strcmp(name, "row_pad")) {                 // doubles, rounded up to whole 128-B lines
         h->row_pad = (int)round_up(std::min<int64_t>(4096, std::max<int64_t>(0, value)), 16);
@@ -602,6 +621,7 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
         return ARIMA_OK;
     }
     if (!strcmp(name, "host_chunk")) { h->host_chunk = std::max<int64_t>(1, value); return ARIMA_OK; }
+    if (!strcmp(name, "host_tail")) { h->host_tail = value ? 1 : 0; return ARIMA_OK; }
     if (!strcmp(name, "host_copy_threads")) {
         h->host_copy_threads = (int)std::min<int64_t>(64, std::max<int64_t>(0, value));
         return ARIMA_OK;
@@ -621,7 +641,7 @@ int arima_get_option(const arima_handle *hc, const char *name, int64_t *value) {
         {"hr_grid", h->hr_grid}, {"row_pad", h->row_pad}, {"bobyqa_wave", h->bobyqa_wave}, {"merge_live", h->merge_live},
         {"search_express_blocks", h->search_express_blocks}, {"donate_evals", h->donate_evals},
         {"donate_evals_drained", h->donate_evals_drained}, {"fuse_diff", h->no_fuse ? 0 : 1}, {"autofit_slice", h->autofit_slice},
-        {"host_copy_threads", h->host_copy_threads}};
+        {"host_copy_threads", h->host_copy_threads}, {"chain_overhead", h->chain_overhead}, {"host_tail", h->host_tail}};
     for (const auto &o : opts)
         if (!strcmp(name, o.n)) {
             *value = o.v;
@@ -750,6 +770,7 @@ static int fit_kernels(arima_handle *h, FitWs &ws, const double *y, int64_t ldn,
     prep.v44 = (unsigned long long)std::max(h->merge_live, 0);
     prep.v45 = (unsigned long long)std::max(h->donate_evals, 0);
     prep.v46 = (unsigned long long)std::max(h->donate_evals_drained, 0);
+    prep.v47 = (unsigned long long)std::max(h->chain_overhead, 0);
     const bool cg = !(p > 0 && q == 0) && method == ARIMA_METHOD_CSS_CGD && k > 0;
     const bool gen = sts::gen_order(p, q);                     // above the compiled orders: arima_generic.hip
     if (!cg || gen) prep.xready_words = 0;                     // no express ring: only the counters are read
@@ -1224,7 +1245,19 @@ int arima_fit_batch(arima_handle *h, const double *series, int64_t N, int32_t T,
     const int k = I + p + q;
     const int P = h->host_pipeline;
     const int64_t chunk = std::min<int64_t>(h->host_chunk, N);
-    const int64_t nchunks = (N + chunk - 1) / chunk;
+    // Chunk boundaries: full chunks, then the last two chunks' worth halved again and again (down to 16 384 series).
+    // The call ends with the fit of its last chunk, whose duration is that chunk's slowest series: a small last chunk
+    // exposes less of it after the final upload (C2 1M x 1024 on 8 queues: profiles/r06/g_e2e, h_e2e)
+    std::vector<int64_t> starts;
+    for (int64_t f = 0; f < N;) {
+        starts.push_back(f);
+        const int64_t rem = N - f;
+        int64_t n = std::min(chunk, rem);
+        if (h->host_tail && rem <= 2 * chunk && rem > arima_handle::kHostTailMin) n = std::max<int64_t>(arima_handle::kHostTailMin, (rem + 1) / 2);
+        f += n;
+    }
+    starts.push_back(N);
+    const int64_t nchunks = (int64_t)starts.size() - 1;
     const int used = (int)std::min<int64_t>(P, nchunks);
     const HostOut o{coef_out, css_ll_out, status_out, n_eval_out, n_grad_out, flags_out};
     h->host_acc = arima_fit_stats{};
@@ -1257,7 +1290,7 @@ int arima_fit_batch(arima_handle *h, const double *series, int64_t N, int32_t T,
         FitCtx &c = h->fctx[ci];
         rc = drain_chunk(h, c, k, o);                       // chunk j - P
         if (rc != ARIMA_OK) break;
-        const int64_t first = j * chunk, n = std::min(chunk, N - first);
+        const int64_t first = starts[j], n = starts[j + 1] - starts[j];
         hipStream_t s = c.stream;
         begin_fit(h, c, s);
         if (T > 0) RCCHK(h, upload_staged(h, c.d_series.ptr, series + first * T, (size_t)n * T * sizeof(double), s),
@@ -1793,9 +1826,10 @@ static int autofit_slice(arima_handle *h, const double *d_series, int64_t N, int
     RCCHK(h, h->af_flags.ensure((size_t)rows_max), "autofit workspace");
     RCCHK(h, h->af_init.ensure((size_t)rows_max * 11 * sizeof(double)), "autofit workspace");
     RCCHK(h, h->af_hrst.ensure((size_t)rows_max * sizeof(int32_t)), "autofit workspace");
-    RCCHK(h, h->af_rlist.ensure((size_t)rows_max * sizeof(int32_t)), "autofit workspace");
-    RCCHK(h, h->af_rcount.ensure(sizeof(unsigned)), "autofit workspace");
-    if (!h->af_host && hipHostMalloc((void **)&h->af_host, (2 * sts::kAfCombosMax + 1) * sizeof(int64_t), 0) != hipSuccess)
+    RCCHK(h, h->af_rlist.ensure((size_t)sts::kBqRefitBuckets * rows_max * sizeof(int32_t)), "autofit workspace");
+    RCCHK(h, h->af_rcount.ensure(sts::kBqRefitBuckets * sizeof(unsigned)), "autofit workspace");
+    if (!h->af_host && hipHostMalloc((void **)&h->af_host, (2 * sts::kAfCombosMax + sts::kBqRefitBuckets) * sizeof(int64_t),
+                                     0) != hipSuccess)
         return set_err(h, ARIMA_E_OOM, "pinned");
     if (!h->ev_af) HIPCHK(h, hipEventCreateWithFlags(&h->ev_af, hipEventDisableTiming));
     const int P = std::min(kAfContexts, kMaxPipeline);
@@ -1875,21 +1909,35 @@ static int autofit_slice(arima_handle *h, const double *d_series, int64_t N, int
         }
         for (int j = 0; j < std::min(used, P); ++j) HIPCHK(h, hipStreamWaitEvent(s, h->fctx[j].ev_done, 0));
         // fitTryBothStrategies (:315-319): every row of the round whose css-cgd fit threw in the optimizer, refitted
-        // with css-bobyqa from the same Hannan-Rissanen init, in place -- one launch for all the round's orders, sized
-        // by the retry count read back (one workgroup per retry, not per candidate row)
+        // with css-bobyqa from the same Hannan-Rissanen init, in place. The rows are listed per dimension k, the host
+        // reads the counts back, and each dimension present runs as one kernel sized by its count (one workgroup per
+        // retry, not per candidate row), the dimensions on different streams so they run together
         RCCHK(h, sts::launch_bobyqa_refit_list(h->af_off.as<int64_t>(), ncombos, total, h->af_status.as<int32_t>(),
-                                               h->af_rlist.as<int32_t>(), h->af_rcount.as<unsigned>(), s), "bobyqa list");
-        HIPCHK(h, hipMemcpyAsync(h->af_host + 2 * sts::kAfCombosMax, h->af_rcount.ptr, sizeof(unsigned),
-                                 hipMemcpyDeviceToHost, s));
+                                               h->af_rlist.as<int32_t>(), rows_max, h->af_rcount.as<unsigned>(), s),
+              "bobyqa list");
+        HIPCHK(h, hipMemcpyAsync(h->af_host + 2 * sts::kAfCombosMax, h->af_rcount.ptr,
+                                 sts::kBqRefitBuckets * sizeof(unsigned), hipMemcpyDeviceToHost, s));
         HIPCHK(h, hipStreamSynchronize(s));
-        unsigned retries = 0;
-        memcpy(&retries, h->af_host + 2 * sts::kAfCombosMax, sizeof retries);
-        RCCHK(h, sts::launch_bobyqa_refit_rows(h->af_rows.as<double>(), ldT, T, h->af_lists.as<int32_t>(), N,
-                                               h->af_off.as<int64_t>(), ncombos, 11, h->af_rlist.as<int32_t>(),
-                                               h->af_rcount.as<unsigned>(), (int64_t)retries, h->af_init.as<double>(),
-                                               h->af_hrst.as<int32_t>(), h->af_coef.as<double>(),
-                                               h->af_ll.as<double>(), h->af_status.as<int32_t>(),
-                                               h->af_flags.as<uint8_t>(), h->bobyqa_wave != 0, s), "bobyqa refit");
+        unsigned retries[sts::kBqRefitBuckets];
+        memcpy(retries, h->af_host + 2 * sts::kAfCombosMax, sizeof retries);
+        HIPCHK(h, hipEventRecord(h->ev_af, s));
+        int launched = 0;
+        for (int k = 2; k < sts::kBqRefitBuckets; ++k) {
+            if (retries[k] == 0) continue;
+            FitCtx &c = h->fctx[launched % P];
+            HIPCHK(h, hipStreamWaitEvent(c.stream, h->ev_af, 0));
+            RCCHK(h, sts::launch_bobyqa_refit_dim(k, h->af_rows.as<double>(), ldT, T, h->af_lists.as<int32_t>(), N,
+                                                  h->af_off.as<int64_t>(), ncombos, 11,
+                                                  h->af_rlist.as<int32_t>() + (int64_t)k * rows_max,
+                                                  h->af_rcount.as<unsigned>(), (int64_t)retries[k],
+                                                  h->af_init.as<double>(), h->af_hrst.as<int32_t>(),
+                                                  h->af_coef.as<double>(), h->af_ll.as<double>(),
+                                                  h->af_status.as<int32_t>(), h->af_flags.as<uint8_t>(),
+                                                  h->bobyqa_wave != 0, c.stream), "bobyqa refit");
+            HIPCHK(h, end_fit(c, c.stream));
+            ++launched;
+        }
+        for (int j = 0; j < std::min(launched, P); ++j) HIPCHK(h, hipStreamWaitEvent(s, h->fctx[j].ev_done, 0));
         RCCHK(h, sts::launch_af_update(N, st, h->af_off.as<int64_t>(), h->af_coef.as<double>(), h->af_ll.as<double>(),
                                        h->af_status.as<int32_t>(), h->af_flags.as<uint8_t>(), h->af_best.as<double>(),
                                        max_p, max_q, s), "autofit update");
