@@ -63,13 +63,9 @@ extern "C" {
 /* ARIMA.autoFit outcomes (ARIMA.scala:280-375), arima_autofit_batch* only */
 #define ARIMA_ST_NOT_STATIONARY     11  /* no d <= max_d passes the KPSS test: "stationarity not achieved", :293-296 */
 #define ARIMA_ST_NO_MODEL           12  /* no candidate qualified: curBestModel stays null (NullPointerException)  */
-#define ARIMA_ST_FALLBACK_UNPINNED  13  /* result returned, but a candidate's css-bobyqa retry (fitTryBothStrategies,
-                                           :315-319) reached BOBYQA's RESCUE branch, which is not restated: that
-                                           candidate counts as failed, so the selection is unpinned                */
+/* 13 and 15 are retired: they reported BOBYQA's RESCUE branch before it was restated (round 6); never returned */
 /* css-bobyqa outcomes (ARIMA.fitWithCSSBOBYQA, ARIMA.scala:130-160) */
 #define ARIMA_ST_TOO_FEW_PARAMS     14  /* BOBYQAOptimizer needs >= 2 parameters (NumberIsTooSmallException)    */
-#define ARIMA_ST_BOBYQA_RESCUE      15  /* BOBYQA reached Powell's RESCUE branch (damaged denominator), which this
-                                           build does not restate: the fit stops there, outcome unpinned          */
 
 /* ---- fit methods (ARIMA.scala:105-109) -------------------------------------------------------------- */
 #define ARIMA_METHOD_CSS_CGD     0
@@ -229,8 +225,7 @@ int arima_order_search_batch_device(arima_handle *h, const double *d_series, int
  * invertible fits. max_p <= 8 (any max_q: the walk only meets q <= 2), any series length (KPSS lags above 32 take
  * one pass per lag). order_out N x 4 = (p, d, q, intercept) (-1s when the series has no model),
  * coef_out N x 11 (zero-padded; NaN when none), aic_out N (+inf when none), status_out N: ARIMA_ST_OK,
- * ARIMA_ST_FALLBACK_UNPINNED (result valid, see above), ARIMA_ST_NOT_STATIONARY, ARIMA_ST_NO_MODEL, or the KPSS
- * regression's shape status (T <= 1). n_fits_out (nullable): candidate fits the walk ran for the series.        */
+ * ARIMA_ST_NOT_STATIONARY, ARIMA_ST_NO_MODEL, or the KPSS regression's shape status (T <= 1). n_fits_out (nullable): candidate fits the walk ran for the series.        */
 int arima_autofit_batch(arima_handle *h, const double *series, int64_t n_series, int32_t T, int32_t max_p,
                         int32_t max_d, int32_t max_q, int32_t *order_out, double *coef_out, double *aic_out,
                         int32_t *status_out, int32_t *n_fits_out);

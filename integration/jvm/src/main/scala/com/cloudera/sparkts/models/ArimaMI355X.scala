@@ -52,8 +52,7 @@ object ArimaStatus {
   val OK = 0; val MAX_EVAL = 1; val BRACKET_MAX_EVAL = 2; val MAX_ITER = 3; val SINGULAR = 4
   val NOT_ENOUGH_DATA = 5; val NO_DATA = 6; val BAD_INTERVAL = 7; val ZERO_PARAMS = 8
   val UNSUPPORTED_METHOD = 9; val SERIES_TOO_SHORT = 10
-  val NOT_STATIONARY = 11; val NO_MODEL = 12; val FALLBACK_UNPINNED = 13; val TOO_FEW_PARAMS = 14
-  val BOBYQA_RESCUE = 15
+  val NOT_STATIONARY = 11; val NO_MODEL = 12; val TOO_FEW_PARAMS = 14     // 13, 15 retired (RESCUE restated)
 
   def toException(status: Int): Throwable = status match {
     case MAX_EVAL => new TooManyEvaluationsException(10000)                    // MaxEval(10000), ARIMA.scala:196
@@ -69,8 +68,6 @@ object ArimaStatus {
     case NOT_STATIONARY => new Exception("stationarity not achieved with differencing order <= maxD")  // :295
     case NO_MODEL => new NullPointerException()                                // curBestModel == null, :302
     case TOO_FEW_PARAMS => new org.apache.commons.math3.exception.NumberIsTooSmallException(1: Integer, 2: Integer, true)
-    case BOBYQA_RESCUE | FALLBACK_UNPINNED =>
-      new IllegalStateException("BOBYQA's RESCUE branch is not restated by the MI355X engine")
     case other => new IllegalStateException(s"unknown ARIMA status $other")
   }
 }
@@ -174,13 +171,11 @@ object ArimaMI355X {
   }
 
   /** Drop-in for ARIMA.autoFit (ARIMA.scala:280-304): one series, the reference's exceptions. maxP <= 8 (its
-    * css-bobyqa retries have at most 11 parameters). A FALLBACK_UNPINNED result (a retry reached BOBYQA's RESCUE
-    * branch) is returned like OK unless strict = true, which throws -- the policy of the Python mirror's
-    * `autofit(..., strict=False)` (include/sparkts_arima.h). */
-  def autoFit(ts: Vector, maxP: Int = 5, maxD: Int = 2, maxQ: Int = 5, strict: Boolean = false): ARIMAModel = {
+    * css-bobyqa retries have at most 11 parameters). */
+  def autoFit(ts: Vector, maxP: Int = 5, maxD: Int = 2, maxQ: Int = 5): ARIMAModel = {
     val (order, coef, _, status) = autoFitMany(Array(ts.toArray), maxP, maxD, maxQ)
     val st = status(0)
-    if (st != ArimaStatus.OK && !(st == ArimaStatus.FALLBACK_UNPINNED && !strict)) throw ArimaStatus.toException(st)
+    if (st != ArimaStatus.OK) throw ArimaStatus.toException(st)
     val Array(p, d, q, c) = order(0)
     new ARIMAModel(p, d, q, coef(0).take(p + q + c), c == 1)
   }

@@ -14,8 +14,8 @@
  * TooManyEvaluationsException (commons drops Powell's NF >= MAXFUN return), and BOBYQAOptimizer.setup rejects
  * dimension < 2 (NumberIsTooSmallException).
  *
- * Not restated: Powell's RESCUE (bobyqb label 190, reached only when rounding has damaged an updating denominator);
- * a fit that reaches it stops with ARIMA_ST_BOBYQA_RESCUE.
+ * RESCUE (bobyqb label 190, reached when rounding has damaged an updating denominator) is restated too (bq_rescue);
+ * its evaluations count toward MaxEval like every other (commons drops Powell's NF >= MAXFUN return there as well).
  *
  * Parity pinning: the algorithm is restated from Powell's published Fortran as recalled, not from commons' source
  * (absent here); the only reference pin is ARIMASuite.scala:58-74 (css-bobyqa within 0.1 of css-cgd on the
@@ -546,9 +546,287 @@ static void bq_update(int n, int npt, double *bmat, double *zmat, double *vlag, 
     }
 }
 
+/* ---- RESCUE (bobyqb label 190: rebuild BMAT / ZMAT when rounding has damaged an updating denominator) ------ *
+ * Powell's RESCUE for npt = 2n + 1: XBASE moves to XBASE + XOPT, the interpolation set is replaced by provisional
+ * points along the coordinate directions (PTSAUX, PTSID) whose BMAT / ZMAT are known in closed form, then as many of
+ * the original points as keep the UPDATE denominators healthy are reinstated one by one (the 80-250 loop), and the
+ * objective is evaluated at the provisional points that remain (260-340), each value updating GOPT / HQ / PQ.
+ * PTSAUX(1..2, j) = ptsaux[2 j], ptsaux[2 j + 1]; PTSID holds Powell's encoded doubles (decoded with his truncating
+ * conversions); W(NDIM + k) = w[ndim + k]. Every evaluation counts toward MaxEval like BOBYQB's (commons: the
+ * 10001st throws, Powell's NF >= MAXFUN return is not restated). Returns 0 when an evaluation threw. */
+static int bq_rescue(int n, int npt, bq_obj *ob, double *xbase, double *xpt, double *fval, double *xopt, double *gopt,
+                     double *hq, double *pq, double *bmat, double *zmat, double *sl, double *su, int *nf_io,
+                     double delta, int *kopt_io, double *vlag, double *ptsaux, double *ptsid, double *w) {
+    const int np = n + 1, nptm = npt - np, ndim = npt + n;
+    const double sfrac = 0.5 / (double)np;
+    int kopt = *kopt_io, nf = *nf_io;
+    const int kentry = kopt;
+    (void)kentry;
+    double sumpq = 0.0, winc = 0.0;
+    for (int k = 0; k < npt; k++) {                            /* 10-20: XOPT to the origin, ZMAT = 0 */
+        double distsq = 0.0;
+        for (int j = 0; j < n; j++) {
+            XPT(k, j) = XPT(k, j) - xopt[j];
+            distsq = distsq + XPT(k, j) * XPT(k, j);
+        }
+        sumpq = sumpq + pq[k];
+        w[ndim + k] = distsq;
+        winc = jmax(winc, distsq);
+        for (int j = 0; j < nptm; j++) ZMAT(k, j) = 0.0;
+    }
+    {                                                          /* 30-40: HQ for the shifted XBASE */
+        int ih = 0;
+        for (int j = 0; j < n; j++) {
+            w[j] = 0.5 * sumpq * xopt[j];
+            for (int k = 0; k < npt; k++) w[j] = w[j] + pq[k] * XPT(k, j);
+            for (int i = 0; i <= j; i++) {
+                hq[ih] = hq[ih] + w[i] * xopt[j] + w[j] * xopt[i];
+                ih++;
+            }
+        }
+    }
+    for (int j = 0; j < n; j++) {                              /* 50: shift XBASE, SL, SU, XOPT; PTSAUX; BMAT = 0 */
+        xbase[j] = xbase[j] + xopt[j];
+        sl[j] = sl[j] - xopt[j];
+        su[j] = su[j] - xopt[j];
+        xopt[j] = 0.0;
+        ptsaux[2 * j] = jmin(delta, su[j]);
+        ptsaux[2 * j + 1] = jmax(-delta, sl[j]);
+        if (ptsaux[2 * j] + ptsaux[2 * j + 1] < 0.0) {
+            const double temp = ptsaux[2 * j];
+            ptsaux[2 * j] = ptsaux[2 * j + 1];
+            ptsaux[2 * j + 1] = temp;
+        }
+        if (fabs(ptsaux[2 * j + 1]) < 0.5 * fabs(ptsaux[2 * j])) ptsaux[2 * j + 1] = 0.5 * ptsaux[2 * j];
+        for (int i = 0; i < ndim; i++) BMAT(i, j) = 0.0;
+    }
+    const double fbase = fval[kopt];
+    ptsid[0] = sfrac;                                          /* 60: the provisional points along e_j */
+    for (int j = 0; j < n; j++) {
+        const int jp = j + 1, jpn = jp + n;                    /* 0-based rows of Powell's JP, JPN (jpn < npt) */
+        ptsid[jp] = (double)(j + 1) + sfrac;
+        ptsid[jpn] = (double)(j + 1) / (double)np + sfrac;
+        const double temp = 1.0 / (ptsaux[2 * j] - ptsaux[2 * j + 1]);
+        BMAT(jp, j) = -temp + 1.0 / ptsaux[2 * j];
+        BMAT(jpn, j) = temp + 1.0 / ptsaux[2 * j + 1];
+        BMAT(0, j) = -BMAT(jp, j) - BMAT(jpn, j);
+        ZMAT(0, j) = sqrt(2.0) / fabs(ptsaux[2 * j] * ptsaux[2 * j + 1]);
+        ZMAT(jp, j) = ZMAT(0, j) * ptsaux[2 * j + 1] * temp;
+        ZMAT(jpn, j) = -ZMAT(0, j) * ptsaux[2 * j] * temp;
+    }
+    /* 70: npt = 2n + 1 leaves no further identifiers (K = 2 NP .. NPT is empty) */
+    int nrem = npt, kold = 0, knew = kopt;
+    double beta = 0.0, denom = 0.0;
+    for (;;) {
+        /* 80-110: exchange PTSID(KOLD) with PTSID(KNEW); reinstate the original point KNEW */
+        for (int j = 0; j < n; j++) {
+            const double temp = BMAT(kold, j);
+            BMAT(kold, j) = BMAT(knew, j);
+            BMAT(knew, j) = temp;
+        }
+        for (int j = 0; j < nptm; j++) {
+            const double temp = ZMAT(kold, j);
+            ZMAT(kold, j) = ZMAT(knew, j);
+            ZMAT(knew, j) = temp;
+        }
+        ptsid[kold] = ptsid[knew];
+        ptsid[knew] = 0.0;
+        w[ndim + knew] = 0.0;
+        nrem--;
+        if (knew != kopt) {
+            const double temp = vlag[kold];
+            vlag[kold] = vlag[knew];
+            vlag[knew] = temp;
+            bq_update(n, npt, bmat, zmat, vlag, beta, denom, knew, w);
+            if (nrem == 0) goto done;
+            for (int k = 0; k < npt; k++) w[ndim + k] = fabs(w[ndim + k]);
+        }
+        for (;;) {
+            /* 120-130: the nearest original point not yet tried (W(NDIM+K) > 0) */
+            double dsqmin = 0.0;
+            for (int k = 0; k < npt; k++) {
+                if (w[ndim + k] > 0.0) {
+                    if (dsqmin == 0.0 || w[ndim + k] < dsqmin) {
+                        knew = k;
+                        dsqmin = w[ndim + k];
+                    }
+                }
+            }
+            if (dsqmin == 0.0) goto evaluate;
+            /* 140-160: its W-vector */
+            for (int j = 0; j < n; j++) w[npt + j] = XPT(knew, j);
+            for (int k = 0; k < npt; k++) {
+                double sum = 0.0;
+                if (k == kopt) {
+                } else if (ptsid[k] == 0.0) {
+                    for (int j = 0; j < n; j++) sum = sum + w[npt + j] * XPT(k, j);
+                } else {
+                    const int ip = (int)ptsid[k];
+                    if (ip > 0) sum = w[npt + ip - 1] * ptsaux[2 * (ip - 1)];
+                    const int iq = (int)((double)np * ptsid[k] - (double)(ip * np));
+                    if (iq > 0) {
+                        const int iw = (ip == 0) ? 1 : 0;
+                        sum = sum + w[npt + iq - 1] * ptsaux[2 * (iq - 1) + iw];
+                    }
+                }
+                w[k] = 0.5 * sum * sum;
+            }
+            /* 170-230: VLAG and BETA for reinstating XPT(KNEW, .) */
+            for (int k = 0; k < npt; k++) {
+                double sum = 0.0;
+                for (int j = 0; j < n; j++) sum = sum + BMAT(k, j) * w[npt + j];
+                vlag[k] = sum;
+            }
+            beta = 0.0;
+            for (int j = 0; j < nptm; j++) {
+                double sum = 0.0;
+                for (int k = 0; k < npt; k++) sum = sum + ZMAT(k, j) * w[k];
+                beta = beta - sum * sum;
+                for (int k = 0; k < npt; k++) vlag[k] = vlag[k] + sum * ZMAT(k, j);
+            }
+            double bsum = 0.0, distsq = 0.0;
+            for (int j = 0; j < n; j++) {
+                double sum = 0.0;
+                for (int k = 0; k < npt; k++) sum = sum + BMAT(k, j) * w[k];
+                const int jp = j + npt;
+                bsum = bsum + sum * w[jp];
+                for (int ip = npt; ip < ndim; ip++) sum = sum + BMAT(ip, j) * w[ip];
+                bsum = bsum + sum * w[jp];
+                vlag[jp] = sum;
+                distsq = distsq + XPT(knew, j) * XPT(knew, j);
+            }
+            beta = 0.5 * distsq * distsq + beta - bsum;
+            vlag[kopt] = vlag[kopt] + 1.0;
+            /* 240-250: KOLD, the provisional point whose deletion keeps the denominator largest */
+            denom = 0.0;
+            double vlmxsq = 0.0;
+            for (int k = 0; k < npt; k++) {
+                if (ptsid[k] != 0.0) {
+                    double hdiag = 0.0;
+                    for (int j = 0; j < nptm; j++) hdiag = hdiag + ZMAT(k, j) * ZMAT(k, j);
+                    const double den = beta * hdiag + vlag[k] * vlag[k];
+                    if (den > denom) {
+                        kold = k;
+                        denom = den;
+                    }
+                }
+                vlmxsq = jmax(vlmxsq, vlag[k] * vlag[k]);
+            }
+            if (denom <= 1.0e-2 * vlmxsq) {
+                w[ndim + knew] = -w[ndim + knew] - winc;
+                continue;
+            }
+            break;
+        }
+    }
+evaluate:
+    /* 260-340: the provisional points that remain, each evaluated and folded into the model */
+    for (int kpt = 0; kpt < npt; kpt++) {
+        if (ptsid[kpt] == 0.0) continue;
+        int ih = 0;
+        for (int j = 0; j < n; j++) {
+            w[j] = XPT(kpt, j);
+            XPT(kpt, j) = 0.0;
+            const double temp = pq[kpt] * w[j];
+            for (int i = 0; i <= j; i++) {
+                hq[ih] = hq[ih] + temp * w[i];
+                ih++;
+            }
+        }
+        pq[kpt] = 0.0;
+        const int ip = (int)ptsid[kpt];
+        const int iq = (int)((double)np * ptsid[kpt] - (double)(ip * np));
+        double xp = 0.0, xq = 0.0;
+        if (ip > 0) {
+            xp = ptsaux[2 * (ip - 1)];
+            XPT(kpt, ip - 1) = xp;
+        }
+        if (iq > 0) {
+            xq = ptsaux[2 * (iq - 1)];
+            if (ip == 0) xq = ptsaux[2 * (iq - 1) + 1];
+            XPT(kpt, iq - 1) = xq;
+        }
+        double vquad = fbase;                                  /* the model at the new point */
+        int ihp = 0;
+        if (ip > 0) {
+            ihp = (ip + ip * ip) / 2;                          /* Powell's 1-based packed index */
+            vquad = vquad + xp * (gopt[ip - 1] + 0.5 * xp * hq[ihp - 1]);
+        }
+        if (iq > 0) {
+            const int ihq = (iq + iq * iq) / 2;
+            vquad = vquad + xq * (gopt[iq - 1] + 0.5 * xq * hq[ihq - 1]);
+            if (ip > 0) {
+                const int iw = (ihp > ihq ? ihp : ihq) - abs(ip - iq);
+                vquad = vquad + xp * xq * hq[iw - 1];
+            }
+        }
+        for (int k = 0; k < npt; k++) {
+            double temp = 0.0;
+            if (ip > 0) temp = temp + xp * XPT(k, ip - 1);
+            if (iq > 0) temp = temp + xq * XPT(k, iq - 1);
+            vquad = vquad + 0.5 * pq[k] * temp * temp;
+        }
+        double x[BQ_KMAX], f;                                  /* 290: XBASE + XPT(KPT, .), unbounded */
+        for (int i = 0; i < n; i++) x[i] = xbase[i] + XPT(kpt, i);
+        nf++;
+        if (!bq_eval(ob, x, &f)) {
+            *nf_io = nf;
+            *kopt_io = kopt;
+            return 0;
+        }
+        fval[kpt] = f;
+        if (f < fval[kopt]) kopt = kpt;
+        const double diff = f - vquad;
+        for (int i = 0; i < n; i++) gopt[i] = gopt[i] + diff * BMAT(kpt, i);     /* 310-330: the model update */
+        for (int k = 0; k < npt; k++) {
+            double sum = 0.0;
+            for (int j = 0; j < nptm; j++) sum = sum + ZMAT(k, j) * ZMAT(kpt, j);
+            const double temp = diff * sum;
+            if (ptsid[k] == 0.0) {
+                pq[k] = pq[k] + temp;
+            } else {
+                const int kp = (int)ptsid[k];
+                const int kq = (int)((double)np * ptsid[k] - (double)(kp * np));
+                const int ihq = (kq * kq + kq) / 2;
+                if (kp == 0) {
+                    hq[ihq - 1] = hq[ihq - 1] + temp * (ptsaux[2 * (kq - 1) + 1] * ptsaux[2 * (kq - 1) + 1]);
+                } else {
+                    const int khp = (kp * kp + kp) / 2;
+                    hq[khp - 1] = hq[khp - 1] + temp * (ptsaux[2 * (kp - 1)] * ptsaux[2 * (kp - 1)]);
+                    if (kq > 0) {
+                        hq[ihq - 1] = hq[ihq - 1] + temp * (ptsaux[2 * (kq - 1)] * ptsaux[2 * (kq - 1)]);
+                        const int iw = (khp > ihq ? khp : ihq) - abs(kq - kp);
+                        hq[iw - 1] = hq[iw - 1] + temp * ptsaux[2 * (kp - 1)] * ptsaux[2 * (kq - 1)];
+                    }
+                }
+            }
+        }
+        ptsid[kpt] = 0.0;
+    }
+done:
+#ifdef BQ_RESCUE_CHECK_HOOK                                    /* debug builds: the rebuilt model's identities */
+    BQ_RESCUE_CHECK_HOOK(n, npt, xpt, fval, gopt, hq, pq, bmat, zmat, kentry, fbase);
+#endif
+    *nf_io = nf;
+    *kopt_io = kopt;
+    return 1;
+}
+
 /* ---- BOBYQA driver + PRELIM + BOBYQB, unbounded, npt = 2n + 1 ------------------------------------------- *
- * Returns ARIMA_ST_*; x (in: the initial point, out: the optimum), n_eval_out = objective evaluations. */
+ * Returns ARIMA_ST_*; x (in: the initial point, out: the optimum), n_eval_out = objective evaluations;
+ * n_rescue (may be NULL) = how many times BOBYQB entered RESCUE. */
+int orc_bobyqa_ex(const double *y, int len, int p, int q, int I, const double *x0, double *x_out, int *n_eval_out,
+                  int *n_rescue);
+static _Thread_local int bq_last_rescues;                      /* the calling thread's last fit (tests, tools) */
+int orc_bobyqa_last_rescues(void) { return bq_last_rescues; }
+
 int orc_bobyqa(const double *y, int len, int p, int q, int I, const double *x0, double *x_out, int *n_eval_out) {
+    return orc_bobyqa_ex(y, len, p, q, I, x0, x_out, n_eval_out, &bq_last_rescues);
+}
+
+int orc_bobyqa_ex(const double *y, int len, int p, int q, int I, const double *x0, double *x_out, int *n_eval_out,
+                  int *n_rescue) {
+    if (n_rescue) *n_rescue = 0;
     const int n = I + p + q;
     *n_eval_out = 0;
     if (n < 2) return ARIMA_ST_TOO_FEW_PARAMS;                 /* BOBYQAOptimizer.setup: dimension >= 2 */
@@ -763,11 +1041,35 @@ int orc_bobyqa(const double *y, int len, int p, int q, int I, const double *x0, 
             if (ntrits == 0) { state = 210; break; }
             state = 230;
             break;
-        case 190:
-            /* RESCUE: not restated */
-            status = ARIMA_ST_BOBYQA_RESCUE;
-            state = -1;
+        case 190: {
+            nfsav = nf;
+            kbase = kopt;
+            double ptsid[BQ_NPTMAX];
+            if (n_rescue) (*n_rescue)++;
+            if (!bq_rescue(n, npt, &ob, xbase, xpt, fval, xopt, gopt, hq, pq, bmat, zmat, sl, su, &nf, delta, &kopt,
+                           vlag, tw, ptsid, w)) {
+                status = ARIMA_ST_MAX_EVAL;
+                state = -1;
+                break;
+            }
+            /* XOPT now, in case of the branch to 720; GOPT's update follows the branch to 20 */
+            xoptsq = 0.0;
+            if (kopt != kbase) {
+                for (int i = 0; i < n; i++) {
+                    xopt[i] = XPT(kopt, i);
+                    xoptsq = xoptsq + xopt[i] * xopt[i];
+                }
+            }
+            nresc = nf;
+            if (nfsav < nf) {
+                nfsav = nf;
+                state = 20;
+                break;
+            }
+            if (ntrits > 0) { state = 60; break; }
+            state = 210;
             break;
+        }
         case 210:
             bq_altmov(n, npt, xpt, xopt, bmat, zmat, sl, su, kopt, knew, adelt, xnew, xalt, &alpha, &cauchy, tw,
                       tw + n, w);

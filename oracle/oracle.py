@@ -20,7 +20,7 @@ _lib = None
 ST_NAMES = {0: "OK", 1: "MAX_EVAL", 2: "BRACKET_MAX_EVAL", 3: "MAX_ITER", 4: "SINGULAR",
             5: "NOT_ENOUGH_DATA", 6: "NO_DATA", 7: "BAD_INTERVAL", 8: "ZERO_PARAMS",
             9: "UNSUPPORTED_METHOD", 10: "SERIES_TOO_SHORT", 11: "NOT_STATIONARY", 12: "NO_MODEL",
-            13: "FALLBACK_UNPINNED", 14: "TOO_FEW_PARAMS", 15: "BOBYQA_RESCUE"}
+            14: "TOO_FEW_PARAMS"}                          # 13, 15 retired: RESCUE is restated
 
 _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int)
@@ -311,9 +311,6 @@ KPSS_CRITICAL = {0: {0.10: 0.347, 0.05: 0.463, 0.025: 0.574, 0.01: 0.739},      
 # autoFit outcomes beyond fitModel's (include/sparkts_arima.h)
 ST_NOT_STATIONARY = 11      # "stationarity not achieved with differencing order <= maxD" (ARIMA.scala:293-296)
 ST_NO_MODEL = 12            # no candidate qualified: curBestModel stays null (ARIMA.scala:322, :304 -> NPE)
-ST_FALLBACK_UNPINNED = 13   # a candidate's css-bobyqa retry (ARIMA.scala:315-319) reached BOBYQA's RESCUE branch,
-                            # which bobyqa_oracle.c does not restate: that candidate counts as failed
-ST_BOBYQA_RESCUE = 15
 CGD_FALLBACK_STATUSES = (1, 2, 3, 7)   # MaxEval, BracketFinder cap, MaxIter, SearchInterval: thrown by the optimizer
 
 
@@ -348,8 +345,7 @@ def autofit(ts, max_p=5, max_d=2, max_q=5, smear=DEFAULT_SMEAR, trace=None):
       (-2 * logLikelihoodCSS + 2 * (p + q + c), :826-830) is strictly below the incumbent's (starting at
       Double.MaxValue, :323); the new incumbent is the first minimum in candidate order (minBy, :350).
     fitTryBothStrategies (:315-319): when css-cgd throws in the optimizer, the candidate is refitted with css-bobyqa
-    (bobyqa_oracle.c) from the same initial parameters; a retry that reaches BOBYQA's unrestated RESCUE branch counts
-    as failed and the result carries ST_FALLBACK_UNPINNED.
+    (bobyqa_oracle.c, RESCUE included) from the same initial parameters.
     Returns dict(status, order (p, d, q, intercept), coef (11, zero-padded), aic, n_fits)."""
     ts = np.ascontiguousarray(ts, dtype=np.float64)
     out = dict(status=0, order=(-1, -1, -1, -1), coef=np.full(11, np.nan), aic=float("inf"), n_fits=0)
@@ -361,7 +357,6 @@ def autofit(ts, max_p=5, max_d=2, max_q=5, smear=DEFAULT_SMEAR, trace=None):
     start_i = 1 if d <= 1 else 0
     best_aic = 1.7976931348623157e308
     best = None
-    fallback = False
     past = set()
     nxt = [(0, 0, start_i), (2, 2, start_i), (1, 0, start_i), (0, 1, start_i)]
     cache = {}
@@ -374,8 +369,6 @@ def autofit(ts, max_p=5, max_d=2, max_q=5, smear=DEFAULT_SMEAR, trace=None):
                 out["n_fits"] += 1
                 if r["status"] in CGD_FALLBACK_STATUSES and not (p > 0 and q == 0):
                     r = fit(diffed, p, 0, q, I, method=1)          # Try(... "css-bobyqa")
-                    if r["status"] == ST_BOBYQA_RESCUE:
-                        fallback = True
                 cache[(p, q, I)] = r
             r = cache[(p, q, I)]
             if r["status"] != 0 or model_flags(r["coef"], p, q, I) != 3:
@@ -403,5 +396,5 @@ def autofit(ts, max_p=5, max_d=2, max_q=5, smear=DEFAULT_SMEAR, trace=None):
     out["coef"][:] = 0.0
     out["coef"][: p + q + I] = r["coef"]
     out["aic"] = best_aic
-    out["status"] = ST_FALLBACK_UNPINNED if fallback else 0
+    out["status"] = 0
     return out

@@ -197,7 +197,6 @@ __global__ __launch_bounds__(256) void k_af_init(int64_t N, const int32_t *__res
     s.seen = 0ull;
     s.best = -1;
     s.n_fits = 0;
-    s.fallback = 0;
     const int d = dsel[i];
     s.dsel = d;
     if (kpss_status != ARIMA_ST_OK) {                     // kpsstest threw (rows <= regressors): autoFit throws
@@ -265,8 +264,7 @@ __global__ __launch_bounds__(256) void k_af_update(int64_t N, AfSeries *__restri
         const int64_t row = base + s.slot[c];
         const int rs = res_status[row];
         // fitTryBothStrategies (:315-319): a css-cgd optimizer failure was refitted with css-bobyqa (the runtime's
-        // k_bobyqa_fit, in place); a retry that reached BOBYQA's unrestated RESCUE branch makes the selection unpinned
-        if (rs == ARIMA_ST_BOBYQA_RESCUE) s.fallback = 1;
+        // k_bobyqa_fit, in place)
         if (rs != ARIMA_ST_OK) continue;                              // .filter(_.isSuccess), :337
         if (res_flags[row] != (ARIMA_FLAG_STATIONARY | ARIMA_FLAG_INVERTIBLE)) continue;   // :342
         const double aic = -2.0 * res_ll[row] + (double)(2 * (p + q + I));             // approxAIC, :826-830
@@ -316,7 +314,6 @@ __global__ __launch_bounds__(256) void k_af_finish(int64_t N, const AfSeries *__
     int status = s.status;
     if (status == ARIMA_ST_OK && s.best < 0) status = ARIMA_ST_NO_MODEL;     // curBestModel == null -> NPE, :304
     const bool ok = s.best >= 0 && s.status == ARIMA_ST_OK;
-    if (ok && s.fallback) status = ARIMA_ST_FALLBACK_UNPINNED;
     const int pk = s.best;
     order_out[i * 4 + 0] = ok ? (pk & 15) : -1;
     order_out[i * 4 + 1] = ok ? s.dsel : -1;

@@ -5,15 +5,14 @@
 // The reference runs commons-math3 3.4.1's BOBYQAOptimizer (a Java translation of M.J.D. Powell's BOBYQA, 2009) with
 // npt = 2k + 1, rhobeg = min(0.96, 0.2 * max|init|), rhoend = 1e-6 * rhobeg, unbounded, maximising
 // logLikelihoodCSSARMA, MaxEval(10000). k_bobyqa_fit gives every series a lane that runs Powell's routines (PRELIM,
-// BOBYQB, TRSBOX, ALTMOV, UPDATE) for that configuration in their published operation order -- with infinite bounds
-// every bound test is inactive -- and evaluates the objective by streaming its own row (bq_css_ll: the CSS recursion
-// of ARIMA.scala:430-445 / 581-618, css_pass's operations). The interpolation state (XPT, BMAT, ZMAT, the quadratic
-// model: 2.9 KB at k = 5, 6 KB at k = 8) is a BqState<k>.
-// As in the oracle (oracle/bobyqa_oracle.c), Powell's RESCUE is not restated: a fit that reaches it reports
-// ARIMA_ST_BOBYQA_RESCUE. Two layouts, bit-identical: a lane per series (the state in private memory; lanes diverge,
-// every series takes its own trust-region path) for large batches, and a wave per series (the state in LDS, the
-// wave's lanes run one series' uniform code: no divergence, LDS instead of scratch latency) for small batches and
-// autoFit's retries, whose time is set by their slowest series.
+// BOBYQB, TRSBOX, ALTMOV, UPDATE, RESCUE) for that configuration in their published operation order -- with infinite
+// bounds every bound test is inactive -- and evaluates the objective by streaming its own row (bq_css_ll: the CSS
+// recursion of ARIMA.scala:430-445 / 581-618, css_pass's operations). The interpolation state (XPT, BMAT, ZMAT, the
+// quadratic model: 2.9 KB at k = 5, 6 KB at k = 8) is a BqState<k>. RESCUE (bobyqb label 190) follows the oracle's
+// bq_rescue (oracle/bobyqa_oracle.c). Two layouts, bit-identical: a lane per series (the state in private memory;
+// lanes diverge, every series takes its own trust-region path) for large batches, and a wave per series (the state in
+// LDS, the wave's lanes run one series' uniform code: no divergence, LDS instead of scratch latency) for small batches
+// and autoFit's retries, whose time is set by their slowest series.
 #include <algorithm>
 
 #include "arima_device.hpp"
@@ -686,6 +685,264 @@ __device__ __forceinline__ void bq_update(double *bmat, double *zmat, double *vl
     (void)par;
 }
 
+/* ---- RESCUE, its first part (labels 10-250: no evaluations) -------------------------------------------------- *
+ * Powell's RESCUE as bobyqa_oracle.c bq_rescue restates it, up to label 260: XBASE moves to XBASE + XOPT, the
+ * provisional points along the coordinate directions (PTSAUX = ptsaux[2 j], ptsaux[2 j + 1]; PTSID = Powell's
+ * encoded doubles) replace the interpolation set in BMAT / ZMAT, and the original points that keep the UPDATE
+ * denominators healthy are reinstated. W(NDIM + k) = w[ndim + k]. bq_fit runs 260-340 (one evaluation per
+ * provisional point left) in its own loop so the evaluations stay at its single evaluation site. Rare (a damaged
+ * denominator): the scalar code, which every lane of a wave runs alike in the wave layout. */
+template <int NN, bool WAVE = false>
+__device__ __noinline__ void bq_rescue_setup(BqState<NN> &S, int kopt, double delta, double *ptsaux, double *ptsid) {
+    constexpr int n = NN, npt = 2 * NN + 1, np = n + 1, nptm = npt - np, ndim = npt + n;
+    const double sfrac = 0.5 / (double)np;
+    double *xbase = S.xbase, *xpt = S.xpt, *xopt = S.xopt, *hq = S.hq, *pq = S.pq, *bmat = S.bmat, *zmat = S.zmat,
+           *sl = S.sl, *su = S.su, *vlag = S.vlag, *w = S.w;
+    double sumpq = 0.0, winc = 0.0;
+    bq_sync<WAVE>();
+    for (int k = 0; k < npt; k++) {                            /* 10-20 */
+        double distsq = 0.0;
+        for (int j = 0; j < n; j++) {
+            XPT(k, j) = XPT(k, j) - xopt[j];
+            distsq = distsq + XPT(k, j) * XPT(k, j);
+        }
+        sumpq = sumpq + pq[k];
+        w[ndim + k] = distsq;
+        winc = bq_jmax(winc, distsq);
+        for (int j = 0; j < nptm; j++) ZMAT(k, j) = 0.0;
+    }
+    {                                                          /* 30-40 */
+        int ih = 0;
+        for (int j = 0; j < n; j++) {
+            w[j] = 0.5 * sumpq * xopt[j];
+            for (int k = 0; k < npt; k++) w[j] = w[j] + pq[k] * XPT(k, j);
+            for (int i = 0; i <= j; i++) {
+                hq[ih] = hq[ih] + w[i] * xopt[j] + w[j] * xopt[i];
+                ih++;
+            }
+        }
+    }
+    for (int j = 0; j < n; j++) {                              /* 50 */
+        xbase[j] = xbase[j] + xopt[j];
+        sl[j] = sl[j] - xopt[j];
+        su[j] = su[j] - xopt[j];
+        xopt[j] = 0.0;
+        ptsaux[2 * j] = bq_jmin(delta, su[j]);
+        ptsaux[2 * j + 1] = bq_jmax(-delta, sl[j]);
+        if (ptsaux[2 * j] + ptsaux[2 * j + 1] < 0.0) {
+            const double temp = ptsaux[2 * j];
+            ptsaux[2 * j] = ptsaux[2 * j + 1];
+            ptsaux[2 * j + 1] = temp;
+        }
+        if (fabs(ptsaux[2 * j + 1]) < 0.5 * fabs(ptsaux[2 * j])) ptsaux[2 * j + 1] = 0.5 * ptsaux[2 * j];
+        for (int i = 0; i < ndim; i++) BMAT(i, j) = 0.0;
+    }
+    ptsid[0] = sfrac;                                          /* 60 (70: nothing left for npt = 2n + 1) */
+    for (int j = 0; j < n; j++) {
+        const int jp = j + 1, jpn = jp + n;
+        ptsid[jp] = (double)(j + 1) + sfrac;
+        ptsid[jpn] = (double)(j + 1) / (double)np + sfrac;
+        const double temp = 1.0 / (ptsaux[2 * j] - ptsaux[2 * j + 1]);
+        BMAT(jp, j) = -temp + 1.0 / ptsaux[2 * j];
+        BMAT(jpn, j) = temp + 1.0 / ptsaux[2 * j + 1];
+        BMAT(0, j) = -BMAT(jp, j) - BMAT(jpn, j);
+        ZMAT(0, j) = sqrt(2.0) / fabs(ptsaux[2 * j] * ptsaux[2 * j + 1]);
+        ZMAT(jp, j) = ZMAT(0, j) * ptsaux[2 * j + 1] * temp;
+        ZMAT(jpn, j) = -ZMAT(0, j) * ptsaux[2 * j] * temp;
+    }
+    int nrem = npt, kold = 0, knew = kopt;
+    double beta = 0.0, denom = 0.0;
+    for (;;) {
+        for (int j = 0; j < n; j++) {                          /* 80-110 */
+            const double temp = BMAT(kold, j);
+            BMAT(kold, j) = BMAT(knew, j);
+            BMAT(knew, j) = temp;
+        }
+        for (int j = 0; j < nptm; j++) {
+            const double temp = ZMAT(kold, j);
+            ZMAT(kold, j) = ZMAT(knew, j);
+            ZMAT(knew, j) = temp;
+        }
+        ptsid[kold] = ptsid[knew];
+        ptsid[knew] = 0.0;
+        w[ndim + knew] = 0.0;
+        nrem--;
+        if (knew != kopt) {
+            const double temp = vlag[kold];
+            vlag[kold] = vlag[knew];
+            vlag[knew] = temp;
+            bq_sync<WAVE>();
+            bq_update<NN, WAVE>(bmat, zmat, vlag, beta, denom, knew, w, S.par);
+            bq_sync<WAVE>();
+            if (nrem == 0) break;
+            for (int k = 0; k < npt; k++) w[ndim + k] = fabs(w[ndim + k]);
+        }
+        bool reinstate = false;
+        for (;;) {
+            double dsqmin = 0.0;                               /* 120-130 */
+            for (int k = 0; k < npt; k++) {
+                if (w[ndim + k] > 0.0) {
+                    if (dsqmin == 0.0 || w[ndim + k] < dsqmin) {
+                        knew = k;
+                        dsqmin = w[ndim + k];
+                    }
+                }
+            }
+            if (dsqmin == 0.0) break;
+            for (int j = 0; j < n; j++) w[npt + j] = XPT(knew, j);   /* 140-160 */
+            for (int k = 0; k < npt; k++) {
+                double sum = 0.0;
+                if (k == kopt) {
+                } else if (ptsid[k] == 0.0) {
+                    for (int j = 0; j < n; j++) sum = sum + w[npt + j] * XPT(k, j);
+                } else {
+                    const int ip = (int)ptsid[k];
+                    if (ip > 0) sum = w[npt + ip - 1] * ptsaux[2 * (ip - 1)];
+                    const int iq = (int)((double)np * ptsid[k] - (double)(ip * np));
+                    if (iq > 0) {
+                        const int iw = (ip == 0) ? 1 : 0;
+                        sum = sum + w[npt + iq - 1] * ptsaux[2 * (iq - 1) + iw];
+                    }
+                }
+                w[k] = 0.5 * sum * sum;
+            }
+            for (int k = 0; k < npt; k++) {                    /* 170-230 */
+                double sum = 0.0;
+                for (int j = 0; j < n; j++) sum = sum + BMAT(k, j) * w[npt + j];
+                vlag[k] = sum;
+            }
+            beta = 0.0;
+            for (int j = 0; j < nptm; j++) {
+                double sum = 0.0;
+                for (int k = 0; k < npt; k++) sum = sum + ZMAT(k, j) * w[k];
+                beta = beta - sum * sum;
+                for (int k = 0; k < npt; k++) vlag[k] = vlag[k] + sum * ZMAT(k, j);
+            }
+            double bsum = 0.0, distsq = 0.0;
+            for (int j = 0; j < n; j++) {
+                double sum = 0.0;
+                for (int k = 0; k < npt; k++) sum = sum + BMAT(k, j) * w[k];
+                const int jp = j + npt;
+                bsum = bsum + sum * w[jp];
+                for (int ip = npt; ip < ndim; ip++) sum = sum + BMAT(ip, j) * w[ip];
+                bsum = bsum + sum * w[jp];
+                vlag[jp] = sum;
+                distsq = distsq + XPT(knew, j) * XPT(knew, j);
+            }
+            beta = 0.5 * distsq * distsq + beta - bsum;
+            vlag[kopt] = vlag[kopt] + 1.0;
+            denom = 0.0;                                       /* 240-250 */
+            double vlmxsq = 0.0;
+            for (int k = 0; k < npt; k++) {
+                if (ptsid[k] != 0.0) {
+                    double hdiag = 0.0;
+                    for (int j = 0; j < nptm; j++) hdiag = hdiag + ZMAT(k, j) * ZMAT(k, j);
+                    const double den = beta * hdiag + vlag[k] * vlag[k];
+                    if (den > denom) {
+                        kold = k;
+                        denom = den;
+                    }
+                }
+                vlmxsq = bq_jmax(vlmxsq, vlag[k] * vlag[k]);
+            }
+            if (denom <= 1.0e-2 * vlmxsq) {
+                w[ndim + knew] = -w[ndim + knew] - winc;
+                continue;
+            }
+            reinstate = true;
+            break;
+        }
+        if (!reinstate) break;
+    }
+    bq_sync<WAVE>();
+}
+
+/* RESCUE 260-280 for provisional point kpt: fold PQ(kpt) into HQ, move XPT(kpt, .) to its new position; returns the
+ * model's value there (VQUAD) */
+template <int NN>
+__device__ __forceinline__ double bq_rescue_point(BqState<NN> &S, int kpt, double fbase, const double *ptsaux,
+                                                  const double *ptsid) {
+    constexpr int n = NN, npt = 2 * NN + 1, np = n + 1;
+    double *xpt = S.xpt, *hq = S.hq, *pq = S.pq, *gopt = S.gopt, *w = S.w;
+    int ih = 0;
+    for (int j = 0; j < n; j++) {
+        w[j] = XPT(kpt, j);
+        XPT(kpt, j) = 0.0;
+        const double temp = pq[kpt] * w[j];
+        for (int i = 0; i <= j; i++) {
+            hq[ih] = hq[ih] + temp * w[i];
+            ih++;
+        }
+    }
+    pq[kpt] = 0.0;
+    const int ip = (int)ptsid[kpt];
+    const int iq = (int)((double)np * ptsid[kpt] - (double)(ip * np));
+    double xp = 0.0, xq = 0.0;
+    if (ip > 0) {
+        xp = ptsaux[2 * (ip - 1)];
+        XPT(kpt, ip - 1) = xp;
+    }
+    if (iq > 0) {
+        xq = ptsaux[2 * (iq - 1)];
+        if (ip == 0) xq = ptsaux[2 * (iq - 1) + 1];
+        XPT(kpt, iq - 1) = xq;
+    }
+    double vquad = fbase;
+    int ihp = 0;
+    if (ip > 0) {
+        ihp = (ip + ip * ip) / 2;
+        vquad = vquad + xp * (gopt[ip - 1] + 0.5 * xp * hq[ihp - 1]);
+    }
+    if (iq > 0) {
+        const int ihq = (iq + iq * iq) / 2;
+        vquad = vquad + xq * (gopt[iq - 1] + 0.5 * xq * hq[ihq - 1]);
+        if (ip > 0) {
+            const int iw = (ihp > ihq ? ihp : ihq) - abs(ip - iq);
+            vquad = vquad + xp * xq * hq[iw - 1];
+        }
+    }
+    for (int k = 0; k < npt; k++) {
+        double temp = 0.0;
+        if (ip > 0) temp = temp + xp * XPT(k, ip - 1);
+        if (iq > 0) temp = temp + xq * XPT(k, iq - 1);
+        vquad = vquad + 0.5 * pq[k] * temp * temp;
+    }
+    return vquad;
+}
+
+/* RESCUE 300-340: F at provisional point kpt folded into GOPT / HQ / PQ; PTSID(kpt) = 0 */
+template <int NN>
+__device__ __forceinline__ void bq_rescue_fold(BqState<NN> &S, int kpt, double diff, const double *ptsaux,
+                                               double *ptsid) {
+    constexpr int n = NN, npt = 2 * NN + 1, np = n + 1, nptm = npt - np;
+    double *hq = S.hq, *pq = S.pq, *gopt = S.gopt, *bmat = S.bmat, *zmat = S.zmat;
+    for (int i = 0; i < n; i++) gopt[i] = gopt[i] + diff * BMAT(kpt, i);
+    for (int k = 0; k < npt; k++) {
+        double sum = 0.0;
+        for (int j = 0; j < nptm; j++) sum = sum + ZMAT(k, j) * ZMAT(kpt, j);
+        const double temp = diff * sum;
+        if (ptsid[k] == 0.0) {
+            pq[k] = pq[k] + temp;
+        } else {
+            const int kp = (int)ptsid[k];
+            const int kq = (int)((double)np * ptsid[k] - (double)(kp * np));
+            const int ihq = (kq * kq + kq) / 2;
+            if (kp == 0) {
+                hq[ihq - 1] = hq[ihq - 1] + temp * (ptsaux[2 * (kq - 1) + 1] * ptsaux[2 * (kq - 1) + 1]);
+            } else {
+                const int khp = (kp * kp + kp) / 2;
+                hq[khp - 1] = hq[khp - 1] + temp * (ptsaux[2 * (kp - 1)] * ptsaux[2 * (kp - 1)]);
+                if (kq > 0) {
+                    hq[ihq - 1] = hq[ihq - 1] + temp * (ptsaux[2 * (kq - 1)] * ptsaux[2 * (kq - 1)]);
+                    const int iw = (khp > ihq ? khp : ihq) - abs(kq - kp);
+                    hq[iw - 1] = hq[iw - 1] + temp * ptsaux[2 * (kp - 1)] * ptsaux[2 * (kq - 1)];
+                }
+            }
+        }
+    }
+    ptsid[kpt] = 0.0;
+}
+
 /* ---- BOBYQA driver + PRELIM + BOBYQB, unbounded, npt = 2n + 1 ------------------------------------------- *
  * Returns ARIMA_ST_*; x (in: the initial point, out: the optimum), n_eval_out = objective evaluations. */
 template <int NN, bool WAVE = false>
@@ -793,6 +1050,8 @@ __device__ __forceinline__ int bq_fit(const double *y, int len, int p, int q, in
            adelt = 0.0, alpha = 0.0, cauchy = 0.0, beta = 0.0, denom = 0.0, vquad = 0.0, diff = 0.0, fopt, densav;
     int state = 20;
     int status = ARIMA_ST_OK;
+    int rk = -1;                                               /* RESCUE's provisional point being evaluated */
+    double rfbase = 0.0, rvquad = 0.0;
     // Every evaluation of BOBYQB happens at ONE point of the loop, after the lane's state machine has run to its next
     // evaluation request (state 360) or to its end: the lanes of a wave take different trust-region paths, and with the
     // evaluation inside the switch a wave paid one full CSS pass per lane per request (the lanes' requests fall on
@@ -909,10 +1168,46 @@ __device__ __forceinline__ int bq_fit(const double *y, int len, int p, int q, in
             if (ntrits == 0) { state = 210; break; }
             state = 230;
             break;
-        case 190:
-            /* RESCUE: not restated */
-            status = ARIMA_ST_BOBYQA_RESCUE;
-            state = -1;
+        case 190:                                                  /* RESCUE (bobyqa_oracle.c bq_rescue) */
+            nfsav = nf;
+            kbase = kopt;
+            rfbase = fval[kopt];
+            bq_rescue_setup<NN, WAVE>(S, kopt, delta, tw, S.par);
+            rk = -1;
+            /* fallthrough */
+        case 193:                                                  /* 260: the next provisional point left */
+            rk++;
+            while (rk < npt && S.par[rk] == 0.0) rk++;
+            if (rk < npt) {
+                rvquad = bq_rescue_point<NN>(S, rk, rfbase, tw, S.par);
+                state = 360;                                       /* evaluated at XBASE + XPT(rk, .) */
+                break;
+            }
+            rk = -1;
+            bq_sync<WAVE>();
+            /* XOPT now, in case of the branch to 720; GOPT's update follows the branch to 20 */
+            xoptsq = 0.0;
+            if (kopt != kbase) {
+                for (int i = 0; i < n; i++) {
+                    xopt[i] = XPT(kopt, i);
+                    xoptsq = xoptsq + xopt[i] * xopt[i];
+                }
+            }
+            nresc = nf;
+            if (nfsav < nf) {
+                nfsav = nf;
+                state = 20;
+                break;
+            }
+            if (ntrits > 0) { state = 60; break; }
+            state = 210;
+            break;
+        case 194:                                                  /* RESCUE 290-340, after the evaluation */
+            nf++;
+            fval[rk] = f;
+            if (f < fval[kopt]) kopt = rk;
+            bq_rescue_fold<NN>(S, rk, f - rvquad, tw, S.par);
+            state = 193;
             break;
         case 210:
             bq_altmov<NN>(xpt, xopt, bmat, zmat, sl, su, kopt, knew, adelt, xnew, xalt, &alpha, &cauchy, tw,
@@ -1320,14 +1615,18 @@ __device__ __forceinline__ int bq_fit(const double *y, int len, int p, int q, in
         }
       }
       if (state < 0) break;
-      /* label 360: the evaluation, the wave's lanes together */
-      for (int i = 0; i < n; i++) x[i] = xbase[i] + xnew[i];       /* min(max(XL, .), XU): unbounded */
+      /* label 360 (or RESCUE's 290): the evaluation, the wave's lanes together */
+      if (rk >= 0) {
+          for (int i = 0; i < n; i++) x[i] = xbase[i] + XPT(rk, i);
+      } else {
+          for (int i = 0; i < n; i++) x[i] = xbase[i] + xnew[i];   /* min(max(XL, .), XU): unbounded */
+      }
       if (!bq_eval<NN>(&ob, x, &f)) {
           status = ARIMA_ST_MAX_EVAL;
           state = -1;
           break;
       }
-      state = 361;
+      state = rk >= 0 ? 194 : 361;
     }
     *n_eval_out = ob.n_eval > ob.max_eval ? ob.max_eval : ob.n_eval;
     if (state == -1) return status;

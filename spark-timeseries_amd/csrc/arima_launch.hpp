@@ -85,7 +85,6 @@ struct AfSeries {                  // one series' walk state (findBestARMAModel'
     int32_t status;                // ARIMA_ST_*
     int32_t best;                  // packed p | q << 4 | I << 8 of curBestModel, -1 = null
     int32_t n_fits;                // candidate fits run so far
-    int32_t fallback;              // a css-bobyqa retry reached the unrestated RESCUE branch
     int32_t ncand;                 // candidates of the current round (0: the walk is over)
     int32_t cand[kAfMaxCand];      // nextParams, packed, deduplicated in first-appearance order
     int32_t slot[kAfMaxCand];      // each candidate's row in its order's list this round

@@ -361,9 +361,7 @@ const char *arima_status_name(int s) {
     case ARIMA_ST_SERIES_TOO_SHORT: return "SERIES_TOO_SHORT";
     case ARIMA_ST_NOT_STATIONARY: return "NOT_STATIONARY";
     case ARIMA_ST_NO_MODEL: return "NO_MODEL";
-    case ARIMA_ST_FALLBACK_UNPINNED: return "FALLBACK_UNPINNED";
     case ARIMA_ST_TOO_FEW_PARAMS: return "TOO_FEW_PARAMS";
-    case ARIMA_ST_BOBYQA_RESCUE: return "BOBYQA_RESCUE";
     default: return "UNKNOWN";
     }
 }

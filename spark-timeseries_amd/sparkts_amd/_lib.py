@@ -31,9 +31,7 @@ ST_UNSUPPORTED_METHOD = 9
 ST_SERIES_TOO_SHORT = 10
 ST_NOT_STATIONARY = 11      # autoFit: no d <= max_d passes KPSS
 ST_NO_MODEL = 12            # autoFit: no candidate qualified
-ST_FALLBACK_UNPINNED = 13   # autoFit: a candidate's css-bobyqa retry reached BOBYQA's unrestated RESCUE branch
 ST_TOO_FEW_PARAMS = 14      # css-bobyqa needs >= 2 parameters (NumberIsTooSmallException)
-ST_BOBYQA_RESCUE = 15       # css-bobyqa reached Powell's RESCUE branch (not restated)
 
 METHOD_CSS_CGD = 0
 METHOD_CSS_BOBYQA = 1

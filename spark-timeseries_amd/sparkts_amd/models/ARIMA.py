@@ -61,17 +61,8 @@ class NullPointerException(ARIMAFitError):
     """autoFit: no candidate model qualified, so `bestModel.p` dereferences null (ARIMA.scala:302-304)."""
 
 
-class FallbackUnpinned(ARIMAFitError):
-    """autoFit: a candidate's css-bobyqa retry (ARIMA.scala:315-319) reached BOBYQA's RESCUE branch, which this build
-    does not restate; the selection it returned counts that candidate as failed."""
-
-
 class NumberIsTooSmallException(ARIMAFitError):
     """css-bobyqa: BOBYQAOptimizer needs at least two parameters."""
-
-
-class BobyqaRescueUnavailable(ARIMAFitError):
-    """css-bobyqa reached Powell's RESCUE branch (a damaged updating denominator), which this build does not restate."""
 
 
 _EXC = {
@@ -87,9 +78,7 @@ _EXC = {
     _lib.ST_SERIES_TOO_SHORT: IndexOutOfBoundsException,
     _lib.ST_NOT_STATIONARY: StationarityNotAchieved,
     _lib.ST_NO_MODEL: NullPointerException,
-    _lib.ST_FALLBACK_UNPINNED: FallbackUnpinned,
     _lib.ST_TOO_FEW_PARAMS: NumberIsTooSmallException,
-    _lib.ST_BOBYQA_RESCUE: BobyqaRescueUnavailable,
 }
 
 
@@ -107,18 +96,14 @@ def _method_code(method):
     return _lib.METHODS[method]
 
 
-def autofit(ts, maxp=5, maxd=2, maxq=5, sc=None, device=None, strict=False):
+def autofit(ts, maxp=5, maxd=2, maxq=5, sc=None, device=None):
     """ARIMA.autoFit (ARIMA.scala:280-375), the reference binding's `autofit` (python/sparkts/models/ARIMA.py:25-60):
-    d from the KPSS test, then the stepwise (p, q, intercept) walk with css-cgd fits. Raises what the reference
-    throws (StationarityNotAchieved, NullPointerException, the KPSS regression's MathIllegalArgumentException). A
-    result whose walk met a css-bobyqa retry in the unrestated RESCUE branch is returned (that candidate counted as
-    failed) unless strict=True, which raises FallbackUnpinned instead."""
+    d from the KPSS test, then the stepwise (p, q, intercept) walk with css-cgd fits and fitTryBothStrategies'
+    css-bobyqa retries. Raises what the reference throws (StationarityNotAchieved, NullPointerException, the KPSS
+    regression's MathIllegalArgumentException)."""
     ts = np.asarray(ts, dtype=np.float64).ravel()
     r = autofit_models(ts[None, :], maxp, maxd, maxq, device=device)
-    st = int(r.status[0])
-    if st != _lib.ST_OK and not (st == _lib.ST_FALLBACK_UNPINNED and not strict):
-        raise_for_status(st)
-    return r.model(0, strict=strict)
+    return r.model(0)
 
 
 class AutoFitBatchResult:
@@ -132,10 +117,8 @@ class AutoFitBatchResult:
         self.n_fits = r["n_fits"]
         self._device = device
 
-    def model(self, i, strict=False):
-        st = int(self.status[i])
-        if st != _lib.ST_OK and not (st == _lib.ST_FALLBACK_UNPINNED and not strict):
-            raise_for_status(st)
+    def model(self, i):
+        raise_for_status(int(self.status[i]))
         p, d, q, I = (int(v) for v in self.order[i])
         return ARIMAModel(p, d, q, self.coefficients[i, :p + q + I], bool(I), device=self._device)
 

@@ -48,7 +48,7 @@ def test_pure_host_entry_points():
     names = [lib.arima_status_name(i).decode() for i in range(16)]
     assert names == ["OK", "MAX_EVAL", "BRACKET_MAX_EVAL", "MAX_ITER", "SINGULAR", "NOT_ENOUGH_DATA", "NO_DATA",
                      "BAD_INTERVAL", "ZERO_PARAMS", "UNSUPPORTED_METHOD", "SERIES_TOO_SHORT", "NOT_STATIONARY",
-                     "NO_MODEL", "FALLBACK_UNPINNED", "TOO_FEW_PARAMS", "BOBYQA_RESCUE"]
+                     "NO_MODEL", "UNKNOWN", "TOO_FEW_PARAMS", "UNKNOWN"]    # 13, 15 retired with RESCUE restated
 
 
 def test_status_codes_match_oracle_numbering():

@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from conftest import GOLDEN
+from conftest import GOLDEN, all_cases, load_case
 from test_gpu_parity import check_fit
 
 pytestmark = pytest.mark.gpu
@@ -82,5 +82,35 @@ def test_bobyqa_layouts_are_transparent(engine):
             engine.set_option("bobyqa_wave", wave)
             af[wave] = engine.autofit(host[:128], 5, 2, 5)
         check_autofit(af[1], af[0], "autofit_layouts")
+    finally:
+        engine.set_option("bobyqa_wave", prev)
+
+
+@pytest.mark.parametrize("name", all_cases("bobyqa_rescue_"))
+def test_bobyqa_rescue_both_layouts_match_oracle(engine, name):
+    # Powell's RESCUE (bobyqb label 190; oracle bq_rescue, device bq_rescue_setup / _point / _fold): every series of
+    # these fixtures enters it (tests/test_oracle_rescue.py); both kernels bit for bit against the fixture
+    meta, arr = load_case(name)
+    prev = engine.get_option("bobyqa_wave")
+    try:
+        for wave in (0, 1):
+            engine.set_option("bobyqa_wave", wave)
+            res = engine.fit_batch(arr["series"], meta["p"], meta["d"], meta["q"], bool(meta["I"]), 1)
+            check_fit(res, arr, f"{name}_wave{wave}")
+    finally:
+        engine.set_option("bobyqa_wave", prev)
+
+
+def test_autofit_rows_that_reach_rescue(engine):
+    # the 15 C2-generator rows whose walk retries a candidate with css-bobyqa into RESCUE (status 13 before round 6),
+    # both retry layouts, against oracle.autofit (fixture autofit_rescue_c2_T1024)
+    from test_gpu_autofit import check_autofit
+    z = np.load(f"{GOLDEN}/autofit_rescue_c2_T1024.npz", allow_pickle=False)
+    exp = {k: z[k] for k in ("order", "coef", "aic", "status", "n_fits")}
+    prev = engine.get_option("bobyqa_wave")
+    try:
+        for wave in (0, 1):
+            engine.set_option("bobyqa_wave", wave)
+            check_autofit(engine.autofit(z["series"], 5, 2, 5), exp, f"autofit_rescue_wave{wave}")
     finally:
         engine.set_option("bobyqa_wave", prev)
