@@ -732,8 +732,19 @@ def run_c5(args, eng, series, N, T, total_series, world, rank, dev, barrier, dis
                     "express_pit_passes": st["express_pit_passes"],
                     "express_wave_passes": st["express_f_passes"] + st["express_g_passes"],
                     "bulk_wave_passes": st["wave_f_passes"] + st["wave_g_passes"] + st["wave_multi_passes"],
-                    "merge": {"series": st.get("merge_series"), "waves": st.get("merge_waves")}, "traffic": None,
-                    "traffic_source": "no PMC record for C5 (216 launches per step)"}
+                    "merge": {"series": st.get("merge_series"), "waves": st.get("merge_waves")}}
+        sha = build_sha()
+        pmc, pmc_key = pmc_traffic({"config": "c5", "series": N, "T": T, "smear": args.smear,
+                                    "options": os.environ.get("SPARKTS_OPTIONS", "")}, sha)
+        roofline.update({
+            "traffic": pmc["hbm_bytes_per_step"] if pmc else None,
+            "traffic_unit": "bytes per search step (HBM read+write of every kernel of the 216 grid fits, rocprofv3 PMC)",
+            "traffic_source": pmc["source"] if pmc else
+            "no rocprofv3 PMC record of this workload for this build (library sha256 " + str(sha)[:16] + ")",
+            "build_sha": sha, "traffic_matched_on": pmc_key,
+            "hbm_GBps_pmc": (pmc["hbm_bytes_per_step"] / (search_ms * 1e-3) / 1e9) if pmc and search_ms else None,
+            "hbm_frac_pmc": (pmc["hbm_bytes_per_step"] / (search_ms * 1e-3) / 1e9 / HBM_PEAK_GBS)
+            if pmc and search_ms else None})
         cpu, parity = None, None
         if world == 1 and args.cpu_seconds > 0:
             cpu, parity = c5_cpu_baseline(series, o, coef, aic, T, args.smear)

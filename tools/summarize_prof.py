@@ -7,7 +7,8 @@ SQ_ACTIVE_* count quad-cycles. Values are per launch (counter sum / launches of 
 usage: python tools/summarize_prof.py gpurun_out [out.txt] [--traffic tools/pmc_traffic_c2.json --source NAME]
                                      [--workload '{"series": ..., "T": ..., "p": .., "d": .., "q": .., "I": .., "smear": ..,
                                                    "fit_kernel": 0, "options": ""}']
-(--traffic adds k_cg_fit's measured HBM bytes per launch, keyed by the workload AND the sha256 of the profiled
+(--traffic adds k_cg_fit's measured HBM bytes per launch -- for a C5 workload ({"config": "c5", ...}) the whole
+ order-search step's bytes -- keyed by the workload AND the sha256 of the profiled
  library spark-timeseries_amd/libsparkts_arima.so, to the record list bench.py reads for roofline.traffic; bench.py
  reports them only for the same workload and build. Default workload: bench.py's C2 run that tools/profile.sh profiles)
 """
@@ -93,6 +94,29 @@ def main():
             lines.append(f"   {name:28s} {mean:18.1f}{extra}")
     txt = "\n".join(lines)
     fit = next((v for k, v in cs.items() if k.startswith("k_cg_fit")), {})
+    if traffic_path and workload.get("config") == "c5":
+        # the order search: one step = every kernel of the 216 grid fits (all k_cg_fit / k_hr_init / k_ar_fit / ...
+        # instantiations), so the record is the whole step's HBM bytes: the sum over every dispatch of the profiled
+        # run (one step, no warmup) except the series sampler that fills the input
+        import json
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                        "spark-timeseries_amd"))
+        from sparkts_amd.buildinfo import library_sha, source_sha
+        rd = sum(sum(c["FETCH_SIZE"]) for k, c in cs.items() if "sample" not in k and "FETCH_SIZE" in c) * 1024 * 2
+        wr = sum(sum(c["WRITE_SIZE"]) for k, c in cs.items() if "sample" not in k and "WRITE_SIZE" in c) * 1024
+        sha = library_sha()
+        out = {"workload": workload, "build_sha": sha, "source_sha": source_sha(),
+               "kernel": "every kernel of one order-search step", "hbm_bytes_per_step": rd + wr, "read_bytes": rd,
+               "write_bytes": wr, "source": source or root}
+        try:
+            recs = json.load(open(traffic_path))
+            recs = recs if isinstance(recs, list) else [recs]
+        except (OSError, ValueError):
+            recs = []
+        recs = [r for r in recs if not (r.get("workload") == workload and r.get("build_sha") == sha)
+                and r.get("build_sha")] + [out]
+        json.dump(recs, open(traffic_path, "w"), indent=1)
+        fit = {}
     if traffic_path and "FETCH_SIZE" in fit and "WRITE_SIZE" in fit:
         import json
         sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
