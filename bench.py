@@ -79,6 +79,7 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md)
 PMC_TRAFFIC_FILE = os.path.join(ROOT, "tools", "pmc_traffic_c2.json")
 LIB_PATH = os.path.join(ROOT, "spark-timeseries_amd", "libsparkts_arima.so")
 SEED = 20261015
+ISO_STEPS = 3              # isolated launches behind roofline.launch_ms (their median)
 
 
 def build_sha():
@@ -545,13 +546,17 @@ def main():
     flops_step, U, G = cg_flops(s0)
     # the last timed step's outputs, kept for the parity checks below (the isolated step may reuse its buffers)
     last = {k: v.clone() for k, v in outs[(calls[0] - 1) % len(outs)].items()}
-    # the dominant kernel's own launch duration: one more step alone on the GPU (fit_pipeline 1), HIP events
+    # the dominant kernel's own launch duration: steps alone on the GPU (fit_pipeline 1), HIP events; the median of
+    # ISO_STEPS launches (one launch alone once read 224 vs 134-142 ms in the warmups: profiles/r06/q_fuse)
     eng.set_option("fit_pipeline", 1)
-    step()
-    eng.synchronize()
-    s1 = eng.stats()
-    if s1["series_done"] != N:
-        raise SystemExit(f"bench.py: the isolated step wrote {s1['series_done']} of {N} results")
+    iso_ms, s1 = [], None
+    for _ in range(ISO_STEPS):
+        step()
+        eng.synchronize()
+        s1 = eng.stats()
+        if s1["series_done"] != N:
+            raise SystemExit(f"bench.py: the isolated step wrote {s1['series_done']} of {N} results")
+        iso_ms.append(s1["ms_cg_fit"])
     eng.set_option("fit_pipeline", args.pipeline)
     # parity of the configuration that was timed: the last pipelined step against the isolated step,
     # every series, bit for bit (max over ranks of the mismatching series)
@@ -561,7 +566,7 @@ def main():
     if iso_mismatch:
         log(f"[rank {rank}] PARITY: {iso_mismatch} series of the timed step differ from the isolated step")
     flops_iso, _, _ = cg_flops(s1)
-    cg_ms = s1["ms_cg_fit"]
+    cg_ms = sorted(iso_ms)[len(iso_ms) // 2]
     achieved_tf = flops_iso / (cg_ms * 1e-3) / 1e12 if cg_ms > 0 else 0.0
     step_tf = flops_step / (elapsed / args.steps) / 1e12
     wave_passes = s0["wave_f_passes"] + s0["wave_g_passes"] + s0["wave_multi_passes"]
@@ -630,11 +635,11 @@ def main():
                                      "cg_fit": s0["ms_cg_fit"]}},
             "roofline": {"bound": "fp64-valu", "kernel": "k_cg_fit", "achieved": achieved_tf,
                          "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved_tf / FP64_PEAK_TFLOPS,
-                         "launch_ms": cg_ms,
+                         "launch_ms": cg_ms, "launch_ms_each": iso_ms,
                          "achieved_source": "algorithmic flops of one k_cg_fit launch (SURVEY.md 8(d): U*S*(2(p+q)+4) "
                                             "+ G*S*(2(p+q)+4+2kq+1+p+q+2k), U and G counted by the kernel) / that "
-                                            "launch's HIP-event duration, the launch alone on the GPU (one extra "
-                                            "step at fit_pipeline 1 after the timed region)",
+                                            "launch's HIP-event duration, the launch alone on the GPU (the median "
+                                            "of three extra steps at fit_pipeline 1 after the timed region)",
                          "U_per_series": U / max(N, 1), "G_per_series": G / max(N, 1),
                          "achieved_pipelined": step_tf,
                          "achieved_pipelined_source": "the timed steps' k_cg_fit algorithmic flops / ms_per_step "

@@ -145,7 +145,8 @@ int         arima_synchronize(arima_handle *h);
  * "search_express_blocks" (express CUs of each concurrent order-search fit, default 0; -1 = as "express_blocks"),
  * "donate_evals" / "donate_evals_drained" (evaluations before a series may move to an express wave, before / after
  * the batch's work counter ran out; 0 = the kernel's 256 / 32), "fuse_diff" (1, default: device fits of d <= 1 read the
- * caller's rows and difference them inside every pass; 0: through a k_difference workspace -- identical results),
+ * caller's rows and difference them inside every pass where that pays -- compiled orders with p + q <= 6, every
+ * runtime order; 2: at every order; 0: always through a k_difference workspace -- identical results),
  * "autofit_slice" (autoFit series per slice of its workspaces, 0 = from free HBM), "host_copy_threads" (host threads
  * that copy arima_fit_batch's rows into pinned blocks for the upload; default 0 = upload from pageable memory through
  * the HIP runtime's staging), "chain_overhead" (k_cg_fit's objective-pass width model; 0 = the kernel's). */

@@ -742,6 +742,15 @@ __device__ __forceinline__ void hh_apply(const HouseholderState<C> &H, int s, do
     }
 }
 
+// the generator's row elements first .. last-1 in order, differenced on the fly when the generator fuses (F) and
+// dd = 1; F = false streams rows that are already differenced (dd a compile-time 0)
+template <class Gen, class Fn>
+__device__ __forceinline__ void gen_stream(const Gen &gen, const double *__restrict__ row, int first, int last,
+                                           Fn &&fn) {
+    if constexpr (Gen::kFuse) stream_row<kPrefetchHR>(row, gen.dd, first, last, fn);
+    else stream_row<kPrefetchHR>(row, 0, first, last, fn);
+}
+
 // One Householder stage S (compile-time, so every reflection index below is a constant).
 template <int C, int S, class Gen>
 __device__ __forceinline__ int ols_stage(Gen &gen, const double *__restrict__ row, int n, int R,
@@ -761,7 +770,7 @@ __device__ __forceinline__ int ols_stage(Gen &gen, const double *__restrict__ ro
             xnorm = (double)R;
         } else if (S + 1 < R) {
             gen.begin(S + 1);
-            stream_row<kPrefetchHR>(row, gen.dd, gen.first_elem(S + 1), n, [&](double v) {
+            gen_stream(gen, row, gen.first_elem(S + 1), n, [&](double v) {
                 double x[C], y;
                 gen.push(v, x, y);
                 hh_apply<C>(H, S, x, y);
@@ -780,7 +789,7 @@ __device__ __forceinline__ int ols_stage(Gen &gen, const double *__restrict__ ro
         dt = 0.0 + ys * vt;
         if (S + 1 < R) {
             gen.begin(S + 1);
-            stream_row<kPrefetchHR>(row, gen.dd, gen.first_elem(S + 1), n, [&](double v) {
+            gen_stream(gen, row, gen.first_elem(S + 1), n, [&](double v) {
                 double x[C], y;
                 gen.push(v, x, y);
                 hh_apply<C>(H, S, x, y);
@@ -838,14 +847,21 @@ __device__ __forceinline__ int stream_ols(Gen &gen, const double *__restrict__ r
 
 // AR(m) regression: row r = [1?, y(r+m-1), ..., y(r)], response y(r+m).  C = INTERCEPT + m.
 // Streaming: row r is completed by element r + m; window w[l] = y(r + m - l), l = 0..m.
-template <int m, int INTERCEPT>
+// F (fused differencing): y may be the caller's raw row, differenced on the fly when dd = 1 (stream_row); F = false
+// reads rows that are already differenced (dd a compile-time 0, no differencing logic) -- k_hr_init's variant for
+// dd = 0, and for the orders whose fused Householder would outgrow the register file (gen_stream, fuse_hr_pays)
+template <int m, int INTERCEPT, bool F = true>
 struct ARGen {
     static constexpr int C = INTERCEPT + m;
     static constexpr bool kOnesFirst = INTERCEPT != 0;       // column 0 = the intercept's ones
+    static constexpr bool kFuse = F;
     const double *__restrict__ y;             // raw row (dd = 1: differenced on the fly) or differenced row (dd = 0)
     int dd = 0;
     double w[m + 1];
-    __device__ __forceinline__ double at(int i) const { return drow_at(y, dd, i); }
+    __device__ __forceinline__ double at(int i) const {
+        if constexpr (F) return drow_at(y, dd, i);
+        else return y[i];
+    }
     __device__ __forceinline__ void row_at(int r, double (&x)[C], double &yv) const {
         if constexpr (INTERCEPT) x[0] = 1.0;
 #pragma unroll
@@ -874,20 +890,24 @@ struct ARGen {
 // Streaming: row r is completed by element e(r) = m + M + r; y window w[l] = y(e(r) - l), l = 0..m+1;
 // errors window ew[l] = errors(r + M - l), l = 1..q; the newest error of row r is errors(r+M-1), which uses
 // y(e(r)-1-m .. e(r)-1) = w[1..m+1].
-template <int P, int Q, int I>
+template <int P, int Q, int I, bool F = true>
 struct HRGen {
     static constexpr int M = (P > Q ? P : Q);
     static constexpr int m = M + 1;
     static constexpr int C = I + P + Q;
     static constexpr int QA = Q > 0 ? Q : 1;
     static constexpr bool kOnesFirst = I != 0;
+    static constexpr bool kFuse = F;          // as ARGen's F
     const double *__restrict__ y;             // raw row (dd = 1: differenced on the fly) or differenced row (dd = 0)
     int dd = 0;
     double a[m];
     double c;
     double w[m + 2];
     double ew[QA + 1];
-    __device__ __forceinline__ double at(int i) const { return drow_at(y, dd, i); }
+    __device__ __forceinline__ double at(int i) const {
+        if constexpr (F) return drow_at(y, dd, i);
+        else return y[i];
+    }
     __device__ __forceinline__ double err_at(int s) const {
         double acc = 0.0;
 #pragma unroll

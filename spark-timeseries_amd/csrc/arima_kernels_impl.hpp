@@ -28,7 +28,11 @@ using IC = std::integral_constant<int, V>;
 // =======================================================================================================
 // Hannan-Rissanen init (ARIMA.scala:216-242)
 // =======================================================================================================
-template <int P, int Q, int I>
+// F: the row generators difference the caller's raw row on the fly (dd = 1, fused differencing); F = false (dd = 0)
+// streams differenced rows with no differencing logic. At high orders the fused generators cost ~110 registers
+// (k_hr_init<5,5,1>: 399 in round 5, 512 + scratch with the runtime dd; C4 0.92 -> 0.77 M series/s,
+// profiles/r06/p_c4fuse), so the runtime fuses only where that pays (fuse_pays, arima_launch.hpp)
+template <int P, int Q, int I, bool F>
 __global__ __launch_bounds__(256) void k_hr_init(const double *__restrict__ y, int64_t ld, int n, int64_t N,
                                                  double *__restrict__ init_out, int32_t *__restrict__ status_out,
                                                  int dd, FitPrep prep) {
@@ -48,14 +52,14 @@ __global__ __launch_bounds__(256) void k_hr_init(const double *__restrict__ y, i
     for (int j = 0; j < KA; ++j) beta[j] = __builtin_nan("");
     if (st == ARIMA_ST_OK) {
         double ab[1 + m];
-        ARGen<m, 1> genA;
+        ARGen<m, 1, F> genA;
         genA.y = row;
-        genA.dd = dd;
+        genA.dd = F ? dd : 0;
         st = stream_ols<1 + m>(genA, row, n, n - m, ab);           // Autoregression.fitModel(y, m)  :225
         if (st == ARIMA_ST_OK) {
-            HRGen<P, Q, I> genB;
+            HRGen<P, Q, I, F> genB;
             genB.y = row;
-            genB.dd = dd;
+            genB.dd = F ? dd : 0;
             genB.c = ab[0];
 #pragma unroll
             for (int j = 0; j < m; ++j) genB.a[j] = ab[1 + j];
@@ -1270,8 +1274,12 @@ int launch_hr_init_P(const double *y, int64_t ld, int n, int64_t N, int q, int I
             const int block = hr_grid > 0 ? 64 : 256;
             const unsigned grid =
                 hr_grid > 0 ? std::min<unsigned>(grid_for(N, 64), (unsigned)hr_grid) : grid_for(N, 256);
-            hipLaunchKernelGGL((k_hr_init<P, Q, II>), dim3(grid), dim3(block), 0, s, y, ld, n, N, init_out,
-                               status_out, dd, prep);
+            if (dd)
+                hipLaunchKernelGGL((k_hr_init<P, Q, II, true>), dim3(grid), dim3(block), 0, s, y, ld, n, N, init_out,
+                                   status_out, dd, prep);
+            else
+                hipLaunchKernelGGL((k_hr_init<P, Q, II, false>), dim3(grid), dim3(block), 0, s, y, ld, n, N,
+                                   init_out, status_out, 0, prep);
             STS_CHECK_LAUNCH();
             return ARIMA_OK;
         });

@@ -133,6 +133,10 @@ constexpr int kFastMaxOrder = 5;   // orders the compile-time kernels cover
 constexpr int kGenMaxOrder = 20;   // p, q <= 20
 constexpr int kGenMaxK = 2 * kGenMaxOrder + 1;
 inline bool gen_order(int p, int q) { return p > kFastMaxOrder || q > kFastMaxOrder; }
+// Fused differencing pays where the fused Householder init keeps its registers (k_hr_init<P, Q, I, true>): C2's
+// (2,1,2)+c gains 7 % from it, C4's (5,1,5)+c loses 6-16 % (profiles/r06/d_ab, p_c4fuse, q_fuse); the compiled orders
+// with p + q <= 6 fuse, the others take the k_difference copy. The runtime-order kernels always fuse.
+inline bool fuse_pays(int p, int q) { return gen_order(p, q) || p + q <= 6; }
 bool gen_orders_ok(int p, int q);
 int launch_gen_hr_init(const double *y, int64_t ld, int n, int64_t N, int p, int q, int I, double *init_out,
                        int32_t *status_out, int dd, const FitPrep &prep, hipStream_t s);

@@ -179,7 +179,7 @@ struct arima_handle {
     int bobyqa_wave = -1;
     // 1: device fits of d <= 1 difference into the k_difference workspace as before round 6 instead of reading the
     // caller's rows (option "fuse_diff" 0; results are identical, tests compare the two)
-    int no_fuse = 0;
+    int fuse_mode = 1;             // option "fuse_diff": 0 never, 1 where it pays (sts::fuse_pays), 2 always
     int64_t last_express = 0;
     int64_t last_grid = 0;
     int search_lanes = 8;          // concurrent fits of the order search (2/4/8: 1269/1303/1408 series/s, profiles/r02/g_c5)
@@ -582,7 +582,7 @@ int arima_set_option(arima_handle *h, const char *name, int64_t value) {
     std::lock_guard<std::mutex> lk(h->mu);
     if (!strcmp(name, "smear")) { h->smear = value ? 1 : 0; return ARIMA_OK; }
     if (!strcmp(name, "bobyqa_wave")) { h->bobyqa_wave = value < 0 ? -1 : (value ? 1 : 0); return ARIMA_OK; }
-    if (!strcmp(name, "fuse_diff")) { h->no_fuse = value ? 0 : 1; return ARIMA_OK; }
+    if (!strcmp(name, "fuse_diff")) { h->fuse_mode = (int)std::min<int64_t>(2, std::max<int64_t>(0, value)); return ARIMA_OK; }
     if (!strcmp(name, "chain_overhead")) { h->chain_overhead = (int)std::min<int64_t>(4096, std::max<int64_t>(0, value)); return ARIMA_OK; }
     if (!strcmp(name, "autofit_slice")) { h->autofit_slice = std::max<int64_t>(0, value); return ARIMA_OK; }
     if (!strcmp(name, "row_pad")) {                 // doubles, rounded up to whole 128-B lines
@@ -638,7 +638,7 @@ int arima_get_option(const arima_handle *hc, const char *name, int64_t *value) {
         {"host_chunk", h->host_chunk}, {"fit_slice_bytes", h->fit_slice_bytes}, {"express_ring", h->express_ring},
         {"hr_grid", h->hr_grid}, {"row_pad", h->row_pad}, {"bobyqa_wave", h->bobyqa_wave}, {"merge_live", h->merge_live},
         {"search_express_blocks", h->search_express_blocks}, {"donate_evals", h->donate_evals},
-        {"donate_evals_drained", h->donate_evals_drained}, {"fuse_diff", h->no_fuse ? 0 : 1}, {"autofit_slice", h->autofit_slice},
+        {"donate_evals_drained", h->donate_evals_drained}, {"fuse_diff", h->fuse_mode}, {"autofit_slice", h->autofit_slice},
         {"host_copy_threads", h->host_copy_threads}, {"chain_overhead", h->chain_overhead}, {"host_tail", h->host_tail}};
     for (const auto &o : opts)
         if (!strcmp(name, o.n)) {
@@ -890,7 +890,8 @@ static int fit_device_locked(arima_handle *h, FitCtx &c, int ci, int reserve, co
     // -- d = 0 as they are, d = 1 differenced inside every pass (arima_device.hpp stream_row) -- instead of a
     // differenced copy written by k_difference (17 GB of HBM traffic per 1M x 1024 fit, a pipeline stage of its own,
     // and an N x T workspace per fit context). d >= 2 and css-bobyqa keep the copy.
-    const bool fused = d <= 1 && (method == ARIMA_METHOD_CSS_CGD || (p > 0 && q == 0)) && !h->no_fuse;
+    const bool fused = d <= 1 && (method == ARIMA_METHOD_CSS_CGD || (p > 0 && q == 0)) &&
+                       (h->fuse_mode == 2 || (h->fuse_mode == 1 && sts::fuse_pays(p, q)));
     const int64_t ldn = fused ? ld : row_stride(h, n);
     const double *rows = fused ? d_series : nullptr;
 

@@ -818,9 +818,10 @@ def test_row_pad_is_transparent(engine):
 @pytest.mark.parametrize("layout", ["aligned", "odd_ld"])
 def test_fused_differencing_is_transparent(engine, pdqi, layout):
     # round 6: device fits of d <= 1 read the caller's rows and difference them inside every pass (HR streams, AR-only
-    # OLS, bulk objective / gradient passes, express staging) instead of a k_difference workspace. Option fuse_diff 0
-    # restores the workspace; results must not move by a bit, for 128-B aligned rows and for rows at any 8-B offset
-    # (ld = T + 3 and a base one element into the allocation), and must equal the oracle.
+    # OLS, bulk objective / gradient passes, express staging) instead of a k_difference workspace. Option fuse_diff:
+    # 2 fuses at every order, 1 (default) where it pays (p + q <= 6), 0 never; results must not move by a bit, for
+    # 128-B aligned rows and for rows at any 8-B offset (ld = T + 3 and a base one element into the allocation), and
+    # must equal the oracle.
     import torch
     p, d, q, I = pdqi
     N, T = 3000, 700
@@ -837,7 +838,7 @@ def test_fused_differencing_is_transparent(engine, pdqi, layout):
     k = p + q + I
     outs = {}
     try:
-        for fuse in (1, 0):
+        for fuse in (2, 1, 0):
             engine.set_option("fuse_diff", fuse)
             r = [torch.empty((N, k), dtype=torch.float64, device=s.device),
                  torch.empty(N, dtype=torch.float64, device=s.device)] + \
@@ -848,10 +849,10 @@ def test_fused_differencing_is_transparent(engine, pdqi, layout):
             outs[fuse] = ([t.cpu().numpy() for t in r], st)
     finally:
         engine.set_option("fuse_diff", 1)
-    (a, sa), (b, sb) = outs[1], outs[0]
-    for x, y in zip(a, b):
-        assert _same(x, y), pdqi
-    assert sa["series_done"] == N and sa["n_eval"] == sb["n_eval"]
+    (a, sa), (b, sb), (c, sc) = outs[2], outs[0], outs[1]
+    for x, y, z in zip(a, b, c):
+        assert _same(x, y) and _same(x, z), pdqi
+    assert sa["series_done"] == N and sa["n_eval"] == sb["n_eval"] == sc["n_eval"]
     rows = np.arange(0, N, 25)
     host = s.cpu().numpy()[rows]
     st_o, coef, ll, cnt = O.fit_batch(host, p, d, q, I)
