@@ -1265,25 +1265,30 @@ inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 
         if (e_ != hipSuccess) return ARIMA_E_DEVICE;                                                       \
     } while (0)
 
-template <int P>
-int launch_hr_init_P(const double *y, int64_t ld, int n, int64_t N, int q, int I, double *init_out,
-                     int32_t *status_out, hipStream_t s, int hr_grid, int dd, const FitPrep &prep) {
+// one fusion variant of k_hr_init for AR order P (instantiated per (P, F) in arima_hr_p<P>_f<F>.hip: the build runs them
+// in parallel)
+template <int P, bool F>
+int launch_hr_init_PF(const double *y, int64_t ld, int n, int64_t N, int q, int I, double *init_out,
+                      int32_t *status_out, hipStream_t s, int hr_grid, int dd, const FitPrep &prep) {
     return with_order(q, [&](auto Qc) {
         return with_bool(I, [&](auto Ic) {
             constexpr int Q = decltype(Qc)::value, II = decltype(Ic)::value;
             const int block = hr_grid > 0 ? 64 : 256;
             const unsigned grid =
                 hr_grid > 0 ? std::min<unsigned>(grid_for(N, 64), (unsigned)hr_grid) : grid_for(N, 256);
-            if (dd)
-                hipLaunchKernelGGL((k_hr_init<P, Q, II, true>), dim3(grid), dim3(block), 0, s, y, ld, n, N, init_out,
-                                   status_out, dd, prep);
-            else
-                hipLaunchKernelGGL((k_hr_init<P, Q, II, false>), dim3(grid), dim3(block), 0, s, y, ld, n, N,
-                                   init_out, status_out, 0, prep);
+            hipLaunchKernelGGL((k_hr_init<P, Q, II, F>), dim3(grid), dim3(block), 0, s, y, ld, n, N, init_out,
+                               status_out, F ? dd : 0, prep);
             STS_CHECK_LAUNCH();
             return ARIMA_OK;
         });
     });
+}
+
+template <int P>
+int launch_hr_init_P(const double *y, int64_t ld, int n, int64_t N, int q, int I, double *init_out,
+                     int32_t *status_out, hipStream_t s, int hr_grid, int dd, const FitPrep &prep) {
+    return dd ? launch_hr_init_PF<P, true>(y, ld, n, N, q, I, init_out, status_out, s, hr_grid, dd, prep)
+              : launch_hr_init_PF<P, false>(y, ld, n, N, q, I, init_out, status_out, s, hr_grid, 0, prep);
 }
 
 template <int P>
@@ -1408,9 +1413,15 @@ int launch_model_flags_P(const double *coef, int64_t N, int q, int I, uint8_t *f
                                               int32_t *, uint8_t *, unsigned long long *, int, int,             \
                                               unsigned char *, unsigned *, int, hipStream_t, int);
 
+#define STS_DECLARE_HR(PP, FF, EXT)                                                                             \
+    EXT template int launch_hr_init_PF<PP, FF>(const double *, int64_t, int, int64_t, int, int, double *,         \
+                                               int32_t *, hipStream_t, int, int, const FitPrep &);
+
 #define STS_DECLARE_P(PP, EXT)                                                                                  \
     STS_DECLARE_CG(PP, false, extern)                                                                           \
     STS_DECLARE_CG(PP, true, extern)                                                                            \
+    STS_DECLARE_HR(PP, false, extern)                                                                           \
+    STS_DECLARE_HR(PP, true, extern)                                                                            \
     EXT template int launch_hr_init_P<PP>(const double *, int64_t, int, int64_t, int, int, double *, int32_t *,  \
                                           hipStream_t, int, int, const FitPrep &);                              \
     EXT template int launch_ar_fit_P<PP>(const double *, int64_t, int, int64_t, int, double *, double *,         \
