@@ -346,8 +346,9 @@ def oracle_row_parity(res, exp):
 
 def end_to_end(eng, series, p, d, q, I, last, barrier, world, dist, max_over_ranks):
     """the same fit from the caller's (pageable) host memory through the blocking host entry
-    point arima_fit_batch -- the rows copied by host threads into pinned blocks and DMA'd while the fits of earlier
-    chunks run, results back through pinned staging into the caller's arrays. Every rank runs it at once on its own
+    point arima_fit_batch -- the rows uploaded chunk by chunk straight from pageable memory (host_copy_threads 0, the
+    default: staging through pinned blocks measured no faster) while the fits of earlier chunks run, results back
+    through pinned staging into the caller's arrays. Every rank runs it at once on its own
     shard (barrier, max over ranks), so at N > 1 the line carries the host DRAM / PCIe contention of N GPUs. One
     warm-up call on the first chunk sizes the staging buffers. The results must equal the device path's (the last
     timed step) bit for bit on every row."""
@@ -374,9 +375,9 @@ def end_to_end(eng, series, p, d, q, I, last, barrier, world, dist, max_over_ran
             "bit_identical_to_device_path": par["every_rank_bit_identical"], "rows_compared": par["oracle_rows"],
             "rows_identical": par["bit_identical"],
             "options": {n: eng.get_option(n) for n in ("host_chunk", "host_pipeline", "host_copy_threads")},
-            "path": "arima_fit_batch on every rank at once: pageable host N x T -> host threads -> pinned blocks -> "
-                    "DMA to HBM (chunks over 3 fit contexts) -> fused differencing / HR / CG fit -> pinned staging "
-                    "-> caller's arrays; value = all ranks' series / the slowest rank's time"}
+            "path": "arima_fit_batch on every rank at once: pageable host N x T -> chunked uploads to HBM (over the "
+                    "host_pipeline fit contexts) -> fused differencing / HR / CG fit -> pinned staging -> caller's "
+                    "arrays; value = all ranks' series / the slowest rank's time"}
 
 
 def main():
