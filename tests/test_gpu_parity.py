@@ -35,7 +35,9 @@ def check_fit(res, exp, ctx):
     assert np.array_equal(res["n_grad"], exp["n_grad"]), f"{ctx}: n_grad"
     if ok.any():
         c, ce = res["coef"][ok], exp["coef"][ok]
-        fin = np.isfinite(ce)                  # a normal return can sit at a NaN point (css-bobyqa on NaN models)
+        # a normal return can sit at a NaN point (css-bobyqa on NaN models): the north_star tolerances below apply to
+        # the finite values; every value, NaN positions included, must still match exactly (_same, after them)
+        fin = np.isfinite(ce)
         assert np.all(np.abs(c - ce)[fin] <= COEF_ATOL), f"{ctx}: coef tolerance"
         ll, lle = res["ll"][ok], exp["ll"][ok]
         lf = np.isfinite(lle)
