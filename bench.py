@@ -428,8 +428,19 @@ def main():
     if world > 1:
         if not args.dry_run:
             torch.cuda.set_device(dev_id)
-        # the data path has no collective; gloo (CPU) carries only the timing barrier and max-reduction
-        dist.init_process_group("gloo")
+        # the data path has no collective; gloo (CPU) carries only the timing barrier and max-reduction. gloo's C++
+        # side prints its connection report to stdout; it goes to stderr here so rank 0's JSON line stays the only
+        # stdout line a driver has to parse
+        sys.stdout.flush()
+        saved_fd = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo")
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved_fd, 1)
+            os.close(saved_fd)
 
     p, d, q, I, T, base, jitter = CONFIGS[args.config]
     if args.steps is None:                  # enough steps that the pipeline's fill is amortised (C2: 3 steps read
